@@ -1,0 +1,307 @@
+/*
+ * ssa_oracle.c -- CPU restatement of libssa's scoring path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libssa_amd/) links,
+ * loads or calls this file.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py use it, and only as the checker.
+ *
+ * It restates, in plain C99, the reference's exact 64-bit semantics:
+ *   - residue alphabets  (reference src/util/util_sequence.c:44-88)
+ *   - DB residue mapping, unknown -> 0      (util_sequence.c:298-318)
+ *   - query mapping, unknown symbols dropped (src/query.c:102-130)
+ *   - score-matrix text parser + constant scoring, default cell -1
+ *                                           (src/matrices.c:335-460)
+ *   - full_sw, int64 Gotoh local alignment  (src/algo/64/smith_waterman_63.c:32-98)
+ *   - full_nw, int64 Gotoh global alignment (src/algo/64/needleman_wunsch_64.c:32-98)
+ *   - bounded min-heap top-k with the reference's tie behaviour
+ *                                           (src/util/minheap.c:50-106, util.h:12)
+ *
+ * Parity of this restatement is pinned two ways (see tests/test_oracle.py):
+ * the known-answer vectors in the reference's own tests, and
+ * fixtures produced by the reference sources themselves, compiled by
+ * oracle/Makefile into oracle/_ref/ (tools/gen_golden.py).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#include <pthread.h>
+
+#define DIM 32
+
+/* ---------------------------------------------------------------- alphabets */
+/* Code order of the reference alphabets (util_sequence.c:40-61 and 63-88). */
+static const char AA_ORDER[] = "-ABCDEFGHIKLMNPQRSTVWXYZU*OJ";
+static const char NT_ORDER[] = "-ACMGRSVTWYHKDBN";
+
+/* Builds the 256-entry ASCII->code map.  AA: '-' is NOT mapped (it is
+ * unknown), letters in either case.  NT: '-' maps to 0, U is T. */
+void oracle_build_map(int nucleotide, signed char out[256]) {
+    for (int c = 0; c < 256; c++) out[c] = -1;
+    const char* order = nucleotide ? NT_ORDER : AA_ORDER;
+    int n = (int)strlen(order);
+    for (int code = 0; code < n; code++) {
+        char ch = order[code];
+        if (ch == '-') {
+            if (nucleotide) out[(unsigned char)'-'] = 0;
+            continue;
+        }
+        out[(unsigned char)ch] = (signed char)code;
+        if (ch >= 'A' && ch <= 'Z') out[(unsigned char)(ch - 'A' + 'a')] = (signed char)code;
+    }
+    if (nucleotide) {
+        out[(unsigned char)'U'] = out[(unsigned char)'T'];
+        out[(unsigned char)'u'] = out[(unsigned char)'T'];
+    }
+}
+
+/* DB mapping: every residue kept, unknown -> 0 (util_sequence.c:298-318).
+ * Returns the number of unknown residues. */
+size_t oracle_map_db(int nucleotide, const char* s, size_t len, uint8_t* out) {
+    signed char map[256];
+    oracle_build_map(nucleotide, map);
+    size_t unknown = 0;
+    for (size_t i = 0; i < len; i++) {
+        signed char m = map[(unsigned char)s[i]];
+        if (m >= 0) out[i] = (uint8_t)m;
+        else { out[i] = 0; unknown++; }
+    }
+    return unknown;
+}
+
+/* Query mapping: unknown symbols are dropped (query.c:102-130).
+ * Returns the mapped length. */
+size_t oracle_map_query(int nucleotide, const char* s, size_t len, uint8_t* out) {
+    signed char map[256];
+    oracle_build_map(nucleotide, map);
+    size_t n = 0;
+    for (size_t i = 0; i < len; i++) {
+        signed char m = map[(unsigned char)s[i]];
+        if (m >= 0) out[n++] = (uint8_t)m;
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------ matrix */
+/* M[x][y] = m[(x<<5)+y]; x = DB residue, y = query residue
+ * (smith_waterman_63.c:57).  Unset cells are -1 (matrices.c:344). */
+void oracle_matrix_reset(int64_t* m) {
+    for (int i = 0; i < DIM * DIM; i++) m[i] = -1;
+}
+
+/* Constant scoring: cells with both codes >= 1 (matrices.c:447-460). */
+void oracle_matrix_constant(int match, int mismatch, int64_t* m) {
+    oracle_matrix_reset(m);
+    for (int a = 1; a < DIM; a++)
+        for (int b = 1; b < DIM; b++)
+            m[(a << 5) + b] = (a == b) ? match : mismatch;
+}
+
+/* One line of the NCBI-style text format (matrices.c:388-437).
+ * Header lines start with blank/tab; symbols are mapped with the AA map
+ * even for nucleotide work (matrices.c:408,418). */
+static void parse_line(const char* line, int* nsym, signed char* order, int64_t* m) {
+    signed char map[256];
+    oracle_build_map(0, map);
+    char c = line[0];
+    if (c == '\n' || c == '#' || c == 0) return;
+    if (c == ' ' || c == '\t') {
+        int k = 0;
+        for (const char* p = line + 1; *p; p++)
+            if (*p != ' ' && *p != '\t' && *p != '\n') { order[k++] = map[(unsigned char)*p]; (*nsym)++; }
+        return;
+    }
+    int a = map[(unsigned char)c];
+    const char* p = line + 1;
+    for (int i = 0; i < *nsym; i++) {
+        char* end;
+        long v = strtol(p, &end, 10);
+        if (end == p) break;
+        int b = order[i];
+        if (a >= 0 && b >= 0 && a < DIM && b < DIM) m[(a << 5) + b] = v;
+        p = end;
+    }
+}
+
+/* Parses a whole matrix text (string or file contents). */
+void oracle_matrix_parse(const char* text, int64_t* m) {
+    oracle_matrix_reset(m);
+    signed char order[4096];
+    int nsym = 0;
+    const char* s = text;
+    char line[4096];
+    while (*s) {
+        const char* nl = strchr(s, '\n');
+        size_t n = nl ? (size_t)(nl - s) : strlen(s);
+        if (n >= sizeof(line)) n = sizeof(line) - 1;
+        memcpy(line, s, n);
+        line[n] = 0;
+        parse_line(line, &nsym, order, m);
+        s = nl ? nl + 1 : s + strlen(s);
+    }
+}
+
+/* --------------------------------------------------------------- scorers */
+/* full_sw restated: column j over DB, row i over query; H,E per row kept in
+ * hearray; F and the diagonal carried down the column; H clamped at 0;
+ * score = max over all cells (smith_waterman_63.c:32-98). */
+int64_t oracle_full_sw(const uint8_t* d, size_t dlen, const uint8_t* q, size_t qlen,
+                       const int64_t* m, int gapO, int gapE, int64_t* hearray) {
+    int64_t s = 0;
+    for (size_t i = 0; i < 2 * qlen; i++) hearray[i] = 0;
+    for (size_t j = 0; j < dlen; j++) {
+        int64_t h = 0, f = 0;
+        int64_t* hep = hearray;
+        const int64_t* row = m + ((size_t)d[j] << 5);
+        for (size_t i = 0; i < qlen; i++) {
+            int64_t n = hep[0];
+            int64_t e = hep[1];
+            h += row[q[i]];
+            if (e > h) h = e;
+            if (f > h) h = f;
+            if (h < 0) h = 0;
+            if (h > s) s = h;
+            hep[0] = h;
+            e += gapE;
+            f += gapE;
+            h += gapO + gapE;
+            if (h > e) e = h;
+            if (h > f) f = h;
+            hep[1] = e;
+            h = n;
+            hep += 2;
+        }
+    }
+    return s;
+}
+
+/* full_nw restated: boundary H(i,-1)=Q+(i+1)R, incoming E at column 0 =
+ * 2Q+(i+2)R; per column F into row 0 = 2Q+(j+2)R and diagonal of row 0 =
+ * H(-1,j-1) (0 for j=0, else Q+jR); score = H(qlen-1, dlen-1)
+ * (needleman_wunsch_64.c:32-98).  qlen must be > 0. */
+int64_t oracle_full_nw(const uint8_t* d, size_t dlen, const uint8_t* q, size_t qlen,
+                       const int64_t* m, int gapO, int gapE, int64_t* hearray) {
+    for (size_t i = 0; i < qlen; i++) {
+        hearray[2 * i] = gapO + (int64_t)(i + 1) * gapE;
+        hearray[2 * i + 1] = 2 * (int64_t)gapO + (int64_t)(i + 2) * gapE;
+    }
+    for (size_t j = 0; j < dlen; j++) {
+        int64_t* hep = hearray;
+        int64_t f = 2 * (int64_t)gapO + (int64_t)(j + 2) * gapE;
+        int64_t h = (j == 0) ? 0 : (gapO + (int64_t)j * gapE);
+        const int64_t* row = m + ((size_t)d[j] << 5);
+        for (size_t i = 0; i < qlen; i++) {
+            int64_t n = hep[0];
+            int64_t e = hep[1];
+            h += row[q[i]];
+            if (f > h) h = f;
+            if (e > h) h = e;
+            hep[0] = h;
+            e += gapE;
+            f += gapE;
+            h += gapO + gapE;
+            if (f < h) f = h;
+            if (e < h) e = h;
+            hep[1] = e;
+            h = n;
+            hep += 2;
+        }
+    }
+    return hearray[2 * qlen - 2];
+}
+
+/* Scores every DB sequence (concatenated codes, offsets[k]..offsets[k+1])
+ * against one query.  algo: 0 = SW, 1 = NW.  Multithreaded, order-free. */
+typedef struct {
+    int algo; const uint8_t* db; const uint64_t* off; size_t nseq;
+    const uint8_t* q; size_t qlen; const int64_t* m; int gO, gE;
+    int64_t* out; size_t begin, end;
+} job_t;
+
+static void* run_job(void* p) {
+    job_t* J = (job_t*)p;
+    int64_t* he = (int64_t*)malloc(sizeof(int64_t) * 2 * (J->qlen + 1));
+    for (size_t k = J->begin; k < J->end; k++) {
+        const uint8_t* d = J->db + J->off[k];
+        size_t dl = (size_t)(J->off[k + 1] - J->off[k]);
+        J->out[k] = J->algo == 0 ? oracle_full_sw(d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he)
+                                 : oracle_full_nw(d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he);
+    }
+    free(he);
+    return NULL;
+}
+
+void oracle_scores(int algo, const uint8_t* db, const uint64_t* offsets, size_t nseq,
+                   const uint8_t* q, size_t qlen, const int64_t* m, int gapO, int gapE,
+                   int64_t* out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((size_t)nthreads > nseq) nthreads = nseq ? (int)nseq : 1;
+    pthread_t th[256];
+    job_t jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    size_t per = (nseq + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        job_t J = {algo, db, offsets, nseq, q, qlen, m, gapO, gapE, out, t * per, (t + 1) * per};
+        if (J.begin > nseq) J.begin = nseq;
+        if (J.end > nseq) J.end = nseq;
+        jobs[t] = J;
+        pthread_create(&th[t], NULL, run_job, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+/* ----------------------------------------------------------------- top-k */
+/* Bounded min-heap with the reference's exact structure (minheap.c:50-91):
+ * sift-up on insert with strict '<'; when full, replace the root only when
+ * root.score < new.score; sift-down picks child c+1 only if strictly
+ * smaller than child c.  Final order: score desc, then db_id desc
+ * (CMP_ASC in util.h:12 sorts descending; minheap.c:93-106). */
+typedef struct { int64_t score; uint64_t id; } ent_t;
+
+static void heap_add(ent_t* a, size_t* count, size_t alloc, ent_t n) {
+    if (alloc == 0) return;
+    if (*count < alloc) {
+        size_t i = (*count)++;
+        while (i > 0) {
+            size_t p = (i - 1) / 2;
+            if (!(n.score < a[p].score)) break;
+            a[i] = a[p];
+            i = p;
+        }
+        a[i] = n;
+    } else if (a[0].score < n.score) {
+        size_t p = 0, c = 1;
+        while (c < *count) {
+            if (c + 1 < *count && a[c + 1].score < a[c].score) c++;
+            if (a[c].score < n.score) a[p] = a[c];
+            else break;
+            p = c;
+            c = 2 * p + 1;
+        }
+        a[p] = n;
+    }
+}
+
+static int ent_cmp(const void* x, const void* y) {
+    const ent_t* a = (const ent_t*)x;
+    const ent_t* b = (const ent_t*)y;
+    if (a->score != b->score) return a->score > b->score ? -1 : 1;
+    if (a->id != b->id) return a->id > b->id ? -1 : 1;
+    return 0;
+}
+
+/* Replays the insertions in the given order (= ascending DB ID for the
+ * 64-bit single-thread reference) and returns the sorted top-k. */
+size_t oracle_topk(const int64_t* scores, const uint64_t* ids, size_t n, size_t k,
+                   int64_t* out_scores, uint64_t* out_ids) {
+    ent_t* a = (ent_t*)malloc(sizeof(ent_t) * (k ? k : 1));
+    size_t count = 0;
+    for (size_t i = 0; i < n; i++) {
+        ent_t e = {scores[i], ids[i]};
+        heap_add(a, &count, k, e);
+    }
+    qsort(a, count, sizeof(ent_t), ent_cmp);
+    for (size_t i = 0; i < count; i++) { out_scores[i] = a[i].score; out_ids[i] = a[i].id; }
+    free(a);
+    return count;
+}

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Generates the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container (needs /root/reference and
+``make -C oracle ref``).  The reference sources are compiled in place into
+oracle/_ref/ref_harness; this script feeds it inputs and stores inputs and
+outputs as data:
+
+  tests/golden/tables.npz      the 8 built-in matrices + both residue maps as
+                               parsed by the reference (matrices.c, util_sequence.c)
+  tests/golden/kat.json        known-answer cases of the reference's own tests
+                                with the full top-k the reference's
+                               64-bit and AVX2 16-bit searches return
+  tests/golden/random_*.npz    seeded synthetic DBs (regenerated from their
+                               parameters by libssa_amd.synthetic) with the
+                               reference's full int64 score vector (full_sw /
+                               full_nw) and its 64-bit top-k for several k
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import pyoracle as po  # noqa: E402
+from libssa_amd import synthetic as syn  # noqa: E402
+
+G = os.path.join(ROOT, "tests", "golden")
+D = os.path.join(G, "data")
+NAMES = ["blosum45", "blosum50", "blosum62", "blosum80", "blosum90", "pam30", "pam70", "pam250"]
+
+# (name, db file, nucleotide, query (file: or str:), scoring, gapO, gapE, k, chunk)
+KATS = [
+    ("libssa_const5_4", "AF091148.fas", True, "file:one_seq.fas", ("const", 5, -4), -4, -2, 5, 1000),
+    ("bigger_AF091148", "AF091148.fas", True, "file:one_seq.fas", ("const", 2, -2), -4, -2, 10, 1000),
+    ("searcher_simple", "short_db.fas", True, "str:AT", ("const", 1, -1), -1, -1, 1, 1),
+    ("searcher_multi", "short_nuc_db.fas", True, "str:ATGCAAATTT", ("const", 1, -1), -1, -1, 8, 8),
+    ("search64_test_fas", "test.fas", True,
+     "str:ATGCCCAAGCTGAATAGCGTAGAGGGGTTTTCATCATTTGAGGACGATGTATAA", ("const", 1, -1), -1, -1, 5, 5),
+    ("searcher_AA_const", "short_AA.fas", False,
+     "str:HPEVYILIIPGFGIISHVVSTYSKKPVFGEISMVYAMASIGLLGFLVWSHHMYIVGLDADTRAYFTSATMIIAIPTGIKI",
+     ("const", 1, -1), -1, -1, 1, 1),
+    ("searcher_AA_blosum62", "short_AA.fas", False,
+     "str:HPEVYILIIPGFGIISHVVSTYSKKPVFGEISMVYAMASIGLLGFLVWSHHMYIVGLDADTRAYFTSATMIIAIPTGIKI",
+     ("builtin", "blosum62"), -1, -1, 1, 1),
+    ("overflow_127", "NP_009305.1.fas", False, "file:NP_009305.1.fas", ("const", 127, -1), -1, -1, 1, 1),
+    ("tmp_fas_8bit", "tmp.fas", True, "str:ATGCAAA", ("const", 1, -1), -1, -1, 1, 1),
+    ("config1_Q3ZAI3", "AF091148.fas", False, "file:Q3ZAI3.fasta", ("builtin", "blosum62"), -11, -1, 10, 1000),
+    ("config1_Q3ZAI3_k300", "AF091148.fas", False, "file:Q3ZAI3.fasta", ("builtin", "blosum62"), -11, -1, 300, 1000),
+    ("nt_file_matrix", "AF091148.fas", True, "file:one_seq.fas", ("file", "nuc_scoring_matrix.txt"), -3, -1, 20, 1000),
+    ("blosum90_file", "AF091148_selection.fas", False, "file:P18080.fasta", ("file", "blosum90.txt"), -10, -1, 15, 1000),
+]
+
+
+def matrix_for(spec, tables):
+    if spec[0] == "const":
+        return po.matrix_constant(spec[1], spec[2])
+    if spec[0] == "builtin":
+        return tables[NAMES.index(spec[1])].copy()
+    return po.matrix_parse(open(os.path.join(D, spec[1]), "rb").read())
+
+
+def query_for(q, nt):
+    if q.startswith("file:"):
+        return po.map_query(po.read_query_fasta(os.path.join(D, q[5:])), nt)
+    return po.map_query(q[4:].encode(), nt)
+
+
+def main():
+    if not po.have_ref():
+        po.build(quiet=False)
+    mats, maps = po.ref_run(po.MODE_TABLES)
+    np.savez(os.path.join(G, "tables.npz"), matrices=mats, maps=maps, names=np.array(NAMES))
+    print("tables: ok")
+
+    kats = []
+    for name, dbf, nt, q, spec, go, ge, k, chunk in KATS:
+        M = matrix_for(spec, mats)
+        qc = query_for(q, nt)
+        seqs = [po.map_db(s, nt) for s in po.read_fasta(os.path.join(D, dbf))]
+        case = {"name": name, "db": dbf, "nucleotide": nt, "query": q, "scoring": list(spec),
+                "gap_open": go, "gap_extend": ge, "k": k, "chunk": chunk}
+        for algo, an in ((0, "sw"), (1, "nw")):
+            hits64, _, ns, _ = po.ref_run(po.MODE_SEARCH64, algo, qc, seqs, M, go, ge, k=k, chunk=chunk)
+            hits16, ovf16, _, _ = po.ref_run(po.MODE_SEARCH16_AVX2, algo, qc, seqs, M, go, ge, k=k, chunk=chunk)
+            case[an + "_64"] = hits64
+            case[an + "_16_avx2"] = hits16
+            case[an + "_16_overflow"] = int(ovf16)
+            case["nseq_nonempty"] = int(ns)
+        kats.append(case)
+        print(name, "sw", case["sw_64"][:3], "nw", case["nw_64"][:3])
+    with open(os.path.join(G, "kat.json"), "w") as f:
+        json.dump(kats, f, indent=1)
+
+    # random synthetic cases: (tag, n, seed, qlen, qseed, matrix, gapO, gapE, plant_every)
+    rnd = [
+        ("small_b62", 3000, 11, 120, 3, "blosum62", -11, -1, 500),
+        ("small_b50", 2500, 12, 333, 4, "blosum50", -10, -2, 700),
+        ("medium_b62", 20000, 42, 400, 7, "blosum62", -11, -1, 2000),
+    ]
+    for tag, n, seed, qlen, qseed, mname, go, ge, plant in rnd:
+        q = syn.protein_query(qlen, qseed)
+        codes, off = syn.protein_db(n, seed, query=q, plant_every=plant, lo=0 if n < 10000 else 16, hi=1200)
+        M = mats[NAMES.index(mname)].copy()
+        out = {"n": n, "seed": seed, "qlen": qlen, "qseed": qseed, "matrix": mname,
+               "gap_open": go, "gap_extend": ge, "plant_every": plant,
+               "lo": 0 if n < 10000 else 16, "hi": 1200}
+        arrays = {}
+        for algo, an in ((0, "sw"), (1, "nw")):
+            sc = po.ref_run(po.MODE_SCORES, algo, q, None, M, go, ge, db_off=(codes, off))
+            arrays[an + "_scores"] = sc
+            out[an + "_sha256"] = hashlib.sha256(sc.astype("<i8").tobytes()).hexdigest()
+            for k in (1, 10, 100, 1000):
+                hits, _, _, _ = po.ref_run(po.MODE_SEARCH64, algo, q, None, M, go, ge, k=k,
+                                           db_off=(codes, off))
+                out[f"{an}_top{k}"] = hits
+        np.savez(os.path.join(G, f"random_{tag}.npz"), meta=np.array(json.dumps(out)), **arrays)
+        print(tag, "ok", out["sw_top10"][:3])
+
+
+if __name__ == "__main__":
+    main()
