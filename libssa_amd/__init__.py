@@ -1,0 +1,212 @@
+"""libssa_amd -- MI355X-native optimal-alignment database search.
+
+Python mirror of the C ABI in ``include/libssa.h`` / ``include/libssa_amd.h``
+(the reference's public API, ``src/libssa.h:122-263``), loaded with ctypes
+from the in-tree ``libssa_amd/lib/libssa_amd.so``.  Function names, argument
+meaning and error behaviour are the reference's: configuration errors end the
+process with status 1 (``fatal``), query-file errors return ``None``.
+
+The library itself holds no Python: the scoring runs in the gfx950 kernels
+of ``csrc/kernels.hip``; there is no CPU fallback, and loading fails loudly
+when the shared library has not been built (``python -m libssa_amd.build``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int8, c_long, c_size_t, c_uint8, \
+    c_uint32, c_uint64, c_int64, c_int32, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libssa_amd.so")
+DB_LIB_PATH = os.path.join(LIB_DIR, "libssa_fasta_db.so")
+
+# ---- constants (libssa.h) ---------------------------------------------------
+BLOSUM45, BLOSUM50, BLOSUM62, BLOSUM80, BLOSUM90 = "blosum45", "blosum50", "blosum62", "blosum80", "blosum90"
+PAM30, PAM70, PAM250 = "pam30", "pam70", "pam250"
+NUCLEOTIDE, AMINOACID, TRANS_QUERY, TRANS_DB, TRANS_BOTH = 0, 1, 2, 3, 4
+FORWARD_STRAND, COMPLEMENTARY_STRAND, BOTH_STRANDS = 1, 2, 3
+BIT_WIDTH_8, BIT_WIDTH_16, BIT_WIDTH_64 = 8, 16, 64
+OUTPUT_SILENT, OUTPUT_ERROR, OUTPUT_WARNING, OUTPUT_INFO = 0, 1, 2, 3
+COMPUTE_SCORE, COMPUTE_ALIGNMENT = 0, 1
+READ_FROM_FILE, READ_FROM_STRING, MATRIX_BUILDIN = 0, 1, 2
+COMPUTE_ON_SSE2, COMPUTE_ON_SSE41, COMPUTE_ON_AVX2 = 0, 1, 2
+SW, NW = 0, 1
+TOPK, LOG = 0, 1
+
+
+class db_seq_t(Structure):
+    _fields_ = [("seq", c_void_p), ("len", c_size_t), ("ID", c_size_t), ("strand", c_int), ("frame", c_int)]
+
+
+class q_seq_t(Structure):
+    _fields_ = [("seq", c_void_p), ("len", c_size_t), ("strand", c_int), ("frame", c_int)]
+
+
+class alignment_t(Structure):
+    _fields_ = [("db_seq", db_seq_t), ("query", q_seq_t), ("alignment", c_char_p), ("alignment_len", c_size_t),
+                ("score", c_long), ("align_q_start", c_size_t), ("align_q_end", c_size_t),
+                ("align_d_start", c_size_t), ("align_d_end", c_size_t)]
+
+
+class alignment_list_t(Structure):
+    _fields_ = [("alignments", POINTER(POINTER(alignment_t))), ("len", c_size_t)]
+
+
+class ssa_hit_t(Structure):
+    _fields_ = [("score", c_int64), ("db_id", c_uint64), ("query_id", c_uint8), ("db_strand", c_uint8),
+                ("db_frame", c_uint8), ("pad", c_uint8 * 5)]
+
+
+class ssa_amd_stats_t(Structure):
+    _fields_ = [("search_ms", c_double), ("kernel_ms", c_double), ("wide_ms", c_double), ("d2h_ms", c_double),
+                ("replay_ms", c_double), ("pack_ms", c_double), ("cells", c_uint64), ("entries", c_uint64),
+                ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
+                ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64)]
+
+
+assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
+assert ctypes.sizeof(alignment_t) == 112 and ctypes.sizeof(alignment_list_t) == 16
+assert ctypes.sizeof(ssa_hit_t) == 24
+
+# every symbol include/*.h declares (checked by tests/test_abi.py)
+EXPORTS = {
+    "libssa_amd.so": ["set_output_mode", "set_simd_compute_mode", "set_chunk_size", "set_thread_count",
+                      "init_score_matrix", "init_constant_scores", "init_gap_penalties", "init_symbol_translation",
+                      "init_db", "init_sequence_fasta", "free_sequence", "sw_align", "nw_align", "free_alignment",
+                      "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
+                      "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
+                      "ssa_amd_replay"],
+    "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
+}
+
+_lib = None
+
+
+def load():
+    """Loads the in-tree shared library (fails loudly if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libssa_amd native library not built: {LIB_PATH} missing "
+                           "(run `python -m libssa_amd.build`)")
+    ctypes.CDLL(DB_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P = c_void_p
+    sig = {
+        "set_output_mode": ([c_int], None), "set_simd_compute_mode": ([c_int], None),
+        "set_chunk_size": ([c_size_t], None), "set_thread_count": ([c_size_t], None),
+        "init_score_matrix": ([c_int, c_char_p], None), "init_constant_scores": ([c_int8, c_int8], None),
+        "init_gap_penalties": ([c_int8, c_int8], None), "init_symbol_translation": ([c_int] * 4, None),
+        "init_db": ([c_char_p], None), "init_sequence_fasta": ([c_int, c_char_p], P),
+        "free_sequence": ([P], None),
+        "sw_align": ([P, c_size_t, c_int, c_int], POINTER(alignment_list_t)),
+        "nw_align": ([P, c_size_t, c_int, c_int], POINTER(alignment_list_t)),
+        "free_alignment": ([POINTER(alignment_list_t)], None), "ssa_exit": ([], None),
+        "ssa_amd_device_count": ([], c_int), "ssa_amd_set_device": ([c_int], None),
+        "ssa_amd_set_id_offset": ([c_size_t], None), "ssa_amd_prepare_db": ([], c_int),
+        "ssa_amd_get_stats": ([POINTER(ssa_amd_stats_t)], None), "ssa_amd_set_option": ([c_char_p, c_long], None),
+        "ssa_amd_search": ([P, c_int, c_size_t, c_int, c_int, POINTER(ssa_hit_t), c_size_t], c_size_t),
+        "ssa_amd_replay": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else s
+
+
+# ---- thin Pythonic layer (same names as the C API) ---------------------------
+def set_output_mode(mode): load().set_output_mode(mode)
+def set_simd_compute_mode(mode): load().set_simd_compute_mode(mode)
+def set_chunk_size(size): load().set_chunk_size(size)
+def set_thread_count(n): load().set_thread_count(n)
+def init_score_matrix(mode, matrix): load().init_score_matrix(mode, _b(matrix))
+def init_constant_scores(match, mismatch): load().init_constant_scores(match, mismatch)
+def init_gap_penalties(gap_open, gap_extend): load().init_gap_penalties(gap_open, gap_extend)
+def init_symbol_translation(t, strands, db_gencode, q_gencode):
+    load().init_symbol_translation(t, strands, db_gencode, q_gencode)
+def init_db(path): load().init_db(_b(path))
+def init_sequence_fasta(mode, s): return load().init_sequence_fasta(mode, _b(s))
+def free_sequence(q): load().free_sequence(q)
+def ssa_exit(): load().ssa_exit()
+
+
+def _unpack(alist):
+    if not alist:
+        return []
+    a = alist.contents
+    out = []
+    for i in range(a.len):
+        x = a.alignments[i].contents
+        out.append({"score": int(x.score), "id": int(x.db_seq.ID), "db_len": int(x.db_seq.len),
+                    "db_strand": x.db_seq.strand, "db_frame": x.db_seq.frame,
+                    "q_len": int(x.query.len), "q_strand": x.query.strand, "q_frame": x.query.frame,
+                    "db_seq": ctypes.string_at(x.db_seq.seq, x.db_seq.len) if x.db_seq.seq else b"",
+                    "alignment": x.alignment.decode() if x.alignment else None})
+    return out
+
+
+def sw_align(q, hitcount, bit_width=BIT_WIDTH_16, align_type=COMPUTE_SCORE):
+    """Returns the reference's alignment list as a list of dicts (freed)."""
+    L = load()
+    al = L.sw_align(q, hitcount, bit_width, align_type)
+    res = _unpack(al)
+    L.free_alignment(al)
+    return res
+
+
+def nw_align(q, hitcount, bit_width=BIT_WIDTH_16, align_type=COMPUTE_SCORE):
+    L = load()
+    al = L.nw_align(q, hitcount, bit_width, align_type)
+    res = _unpack(al)
+    L.free_alignment(al)
+    return res
+
+
+def device_count():
+    return load().ssa_amd_device_count()
+
+
+def set_device(dev): load().ssa_amd_set_device(dev)
+def set_id_offset(off): load().ssa_amd_set_id_offset(off)
+def prepare_db(): return load().ssa_amd_prepare_db()
+def set_option(name, value): load().ssa_amd_set_option(_b(name), value)
+
+
+def stats():
+    s = ssa_amd_stats_t()
+    load().ssa_amd_get_stats(ctypes.byref(s))
+    return {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
+
+
+def search(q, algo, hitcount, bit_width=BIT_WIDTH_16, mode=TOPK, cap=None):
+    """ssa_amd_search: sorted top-k (mode=TOPK) or the shard insertion log
+    (mode=LOG) as a list of (score, global_id, query_id, strand, frame)."""
+    L = load()
+    if cap is None:
+        cap = max(hitcount, 1) if mode == TOPK else max(4 * hitcount + 4096, 65536)
+    buf = (ssa_hit_t * cap)()
+    n = L.ssa_amd_search(q, algo, hitcount, bit_width, mode, buf, cap)
+    return [(buf[i].score, buf[i].db_id, buf[i].query_id, buf[i].db_strand, buf[i].db_frame) for i in range(n)]
+
+
+def replay(log, hitcount):
+    """ssa_amd_replay over a (concatenated) insertion log."""
+    L = load()
+    n = len(log)
+    arr = (ssa_hit_t * max(n, 1))()
+    for i, h in enumerate(log):
+        arr[i].score, arr[i].db_id = int(h[0]), int(h[1])
+        if len(h) > 2:
+            arr[i].query_id, arr[i].db_strand, arr[i].db_frame = int(h[2]), int(h[3]), int(h[4])
+    out = (ssa_hit_t * max(hitcount, 1))()
+    c = L.ssa_amd_replay(arr, n, hitcount, out)
+    return [(out[i].score, out[i].db_id) for i in range(c)]

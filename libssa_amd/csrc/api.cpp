@@ -1,0 +1,315 @@
+// api.cpp -- the exported C ABI: every function of include/libssa.h (the
+// reference's src/libssa.h:122-263, implemented in src/libssa.c) plus the
+// MI355X extensions of include/libssa_amd.h.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "engine.h"
+
+using namespace ssa;
+
+namespace ssa {
+p_query query_from_string(const char* s);
+p_query query_from_file(const char* path);
+}
+
+namespace {
+
+// test_configuration (libssa.c:196-219)
+void test_configuration(p_query q) {
+    if (!cfg().gap_open && !cfg().gap_extend)
+        print_warning("Gap opening and gap extension cost set to zero. Possible error.");
+    if (!matrix().ready) fatal("Scoring not initialized.");
+    if (!q) fatal("Query not initialized.");
+    if (ssa_db_get_sequence_count() == 0) print_warning("Database contains zero sequences. Possible error.");
+    if (!matrix().constant && cfg().symtype == NUCLEOTIDE)
+        fatal("Nucleotide sequences can only be aligned using constant scores.");
+}
+
+void check_width(int bw) {
+    if (bw != BIT_WIDTH_8 && bw != BIT_WIDTH_16 && bw != BIT_WIDTH_64)
+        fatal("\nunknown bit width provided: %d\n\n", bw);
+}
+
+// Feeds every (view, entry) score to the reference heap in the 64-bit
+// single-thread insertion order: ID chunks of chunk_size, and inside a chunk
+// query view by query view, entries in ID order (search_64.c:44-56,
+// db_adapter.c:212-239).  Optionally records the accepted insertions.
+void replay(const SearchScores& sc, const EntryMeta& meta, const std::vector<QueryView>& views, TopK& heap,
+            std::vector<Hit>* log) {
+    const size_t V = sc.views, E = sc.entries;
+    const uint64_t off = cfg().id_offset;
+    auto visit = [&](size_t v, size_t e) {
+        const int64_t s = sc.get(v, e);
+        if (heap.full() && s <= heap.root_score()) return;
+        Hit h{s, meta.id[e] + off, (uint8_t)v, meta.strand[e], meta.frame[e]};
+        if (heap.add(h) && log) log->push_back(h);
+    };
+    (void)views;
+    if (V == 1) {
+        if (sc.wide.empty()) {
+            // hot loop: plain int32 scan with the root cached
+            const int32_t* s32 = sc.s32;
+            for (size_t e = 0; e < E; e++) {
+                if (heap.full() && (int64_t)s32[e] <= heap.root_score()) continue;
+                visit(0, e);
+            }
+        } else {
+            for (size_t e = 0; e < E; e++) visit(0, e);
+        }
+        return;
+    }
+    const uint64_t cs = cfg().chunk_size;
+    size_t e0 = 0;
+    while (e0 < E) {
+        const uint64_t chunk_end = (meta.id[e0] / cs + 1) * cs;
+        size_t e1 = e0;
+        while (e1 < E && meta.id[e1] < chunk_end) e1++;
+        for (size_t v = 0; v < V; v++)
+            for (size_t e = e0; e < e1; e++) visit(v, e);
+        e0 = e1;
+    }
+}
+
+void overflow_counters(const SearchScores& sc, int algo, int bw, uint64_t& o8, uint64_t& o16) {
+    o8 = o16 = 0;
+    if (bw == BIT_WIDTH_64) return;
+    for (size_t v = 0; v < sc.views; v++)
+        for (size_t e = 0; e < sc.entries; e++) {
+            const int64_t s = sc.get(v, e);
+            if (algo == kAlgoSW) {
+                if (bw == BIT_WIDTH_8 && s >= 255) o8++;
+                if (s >= 65535) o16++;
+            } else {
+                if (bw == BIT_WIDTH_8 && (s <= -128 || s >= 127)) o8++;
+                if (s <= -32768 || s >= 32767) o16++;
+            }
+        }
+}
+
+struct SearchResult {
+    std::vector<QueryView> views;
+    std::vector<Hit> hits;      // sorted top-k, or the insertion log
+};
+
+void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {
+    const double t0 = now_ms();
+    check_width(bw);
+    ensure_device_db();
+    R.views = query_views(q);
+    SearchScores sc;
+    device_search(R.views, algo, sc);
+    const double t1 = now_ms();
+    TopK heap(k);
+    replay(sc, device_db().meta, R.views, heap, want_log ? &R.hits : nullptr);
+    if (!want_log) R.hits = heap.sorted();
+    const double t2 = now_ms();
+    uint64_t o8 = 0, o16 = 0;
+    if (bw == BIT_WIDTH_8 || cfg().output_mode >= OUTPUT_INFO) overflow_counters(sc, algo, bw, o8, o16);
+    else if (bw == BIT_WIDTH_16 && algo == kAlgoSW) o16 = sc.wide.size();
+    ssa_amd_stats_t& S = stats();
+    S.overflow_8 = o8;
+    S.overflow_16 = o16;
+    S.replay_ms = t2 - t1;
+    S.search_ms = now_ms() - t0;
+    // m_run's bookkeeping messages (manager.c:147-170)
+    const EntryMeta& M = device_db().meta;
+    const size_t cs = cfg().chunk_size;
+    print_info("Device %d - Processed chunks: %ld and sequences: %ld\n", device_db().device,
+               (long)((M.records + cs - 1) / cs), (long)M.size());
+    if (o8 || o16)
+        print_info("Overflow occurred: %ld sequences were re-aligned with 16 bit, and %ld sequences with 64 bit\n",
+                   (long)o8, (long)o16);
+    if (M.records != M.size())
+        print_warning("# Number of processed sequences differs! Expected: %ld - Actual: %ld\n", (long)M.records,
+                      (long)M.size());
+}
+
+// create_score_alignment_list (aligner.c:62-99): one alignment_t per hit,
+// the DB sequence re-fetched through the plugin as a mapped-code copy, the
+// query borrowed from the p_query.  Note the reference's field swap
+// (aligner.c:76-77): db_seq.strand <- frame, db_seq.frame <- strand.
+p_alignment_list build_list(const SearchResult& R) {
+    p_alignment_list L = (p_alignment_list)malloc(sizeof(alignment_list_t));
+    L->len = R.hits.size();
+    L->alignments = (p_alignment*)malloc(sizeof(p_alignment) * (L->len ? L->len : 1));
+    for (size_t i = 0; i < L->len; i++) {
+        const Hit& h = R.hits[i];
+        p_alignment a = (p_alignment)calloc(1, sizeof(alignment_t));
+        const uint64_t local = h.id - cfg().id_offset;
+        std::vector<uint8_t> codes = fetch_entry_codes(local, h.strand, h.frame);
+        const size_t n = codes.empty() ? 0 : codes.size() - 1;
+        a->db_seq.seq = (char*)malloc(n + 1);
+        if (n) memcpy(a->db_seq.seq, codes.data(), n);
+        a->db_seq.seq[n] = 0;
+        a->db_seq.len = n;
+        a->db_seq.ID = h.id;
+        a->db_seq.strand = h.frame;
+        a->db_seq.frame = h.strand;
+        const QueryView& qv = R.views[h.qid];
+        a->query.seq = qv.cseq;
+        a->query.len = qv.len;
+        a->query.strand = qv.strand;
+        a->query.frame = qv.frame;
+        a->score = (long)h.score;
+        L->alignments[i] = a;
+    }
+    return L;
+}
+
+p_alignment_list align(p_query q, size_t k, int bw, int at, int algo) {
+    test_configuration(q);
+    if (at == COMPUTE_ALIGNMENT) {
+        static bool warned = false;
+        if (!warned) print_warning("COMPUTE_ALIGNMENT: traceback is not implemented yet; returning scores only");
+        warned = true;
+    }
+    SearchResult R;
+    run_search(q, algo, k, bw, false, R);
+    return build_list(R);
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------- technical setup
+void set_output_mode(int mode) { cfg().output_mode = mode; }
+void set_simd_compute_mode(int mode) { (void)mode; }
+void set_chunk_size(size_t size) {
+    if (size == 0) {
+        print_error("Only non zero chunk sizes are allowed. Using the default size of 1000 sequences.", size);
+        size = 1000;
+    }
+    cfg().chunk_size = size;
+}
+void set_thread_count(size_t count) { cfg().thread_count = count; }
+
+// ------------------------------------------------------------ initialisation
+void init_score_matrix(int mode, const char* m) {
+    if (mode == READ_FROM_FILE) matrix_from_file(m);
+    else if (mode == READ_FROM_STRING) matrix_from_string(m);
+    else if (mode == MATRIX_BUILDIN) matrix_builtin(m);
+    else fatal("Unknown mode for reading score matrices: %d", mode);
+}
+
+void init_gap_penalties(const int8_t gapO, const int8_t gapE) {
+    cfg().gap_open = gapO;
+    cfg().gap_extend = gapE;
+}
+
+void init_constant_scores(const int8_t p, const int8_t m) { matrix_constant(p, m); }
+
+// MI355X: validates the NEW type and strands (the reference checks the old
+// global symtype twice, libssa.c:146-151, and so rejects any call made after
+// TRANS_DB/TRANS_BOTH was selected).
+void init_symbol_translation(int type, int strands, int d_gencode, int q_gencode) {
+    if (!gencode_valid(q_gencode)) fatal("Illegal query genetic code specified.");
+    if (!gencode_valid(d_gencode)) fatal("Illegal database genetic code specified.");
+    if (type < 0 || type > 4) fatal("Illegal symbol type specified.");
+    if (strands < 1 || strands > 3) fatal("Illegal strands specified.");
+    cfg().symtype = type;
+    cfg().strands = strands;
+    cfg().q_gencode = q_gencode;
+    cfg().d_gencode = d_gencode;
+    init_translation(q_gencode, d_gencode);
+}
+
+void init_db(const char* db_file) {
+    ssa_db_close();
+    ssa_db_init(db_file);
+    cfg().db_generation++;
+    print_info("DB read %lu sequences\n", (unsigned long)ssa_db_get_sequence_count());
+}
+
+p_query init_sequence_fasta(int mode, const char* s) {
+    if (mode == READ_FROM_FILE) return query_from_file(s);
+    if (mode == READ_FROM_STRING) return query_from_string(s);
+    fatal("Unknown mode for reading query sequences: %d", mode);
+}
+
+void free_sequence(p_query p) { delete p; }
+
+// ------------------------------------------------------------------ searches
+p_alignment_list sw_align(p_query p, size_t hitcount, int bit_width, int align_type) {
+    return align(p, hitcount, bit_width, align_type, kAlgoSW);
+}
+
+p_alignment_list nw_align(p_query p, size_t hitcount, int bit_width, int align_type) {
+    return align(p, hitcount, bit_width, align_type, kAlgoNW);
+}
+
+void free_alignment(p_alignment_list alist) {
+    if (!alist) return;
+    if (alist->alignments) {
+        for (size_t i = 0; i < alist->len; i++) {
+            p_alignment a = alist->alignments[i];
+            if (!a) continue;
+            free(a->db_seq.seq);
+            free(a->alignment);
+            free(a);
+        }
+        free(alist->alignments);
+    }
+    free(alist);
+}
+
+void ssa_exit(void) {
+    matrix_free();
+    ssa_db_close();
+    cfg().db_generation++;
+}
+
+// ------------------------------------------------------------- extensions
+int ssa_amd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void ssa_amd_set_device(int device) { cfg().device = device; }
+void ssa_amd_set_id_offset(size_t offset) { cfg().id_offset = offset; }
+
+int ssa_amd_prepare_db(void) {
+    ensure_device_db();
+    return 0;
+}
+
+void ssa_amd_get_stats(ssa_amd_stats_t* out) {
+    if (out) *out = stats();
+}
+
+void ssa_amd_set_option(const char* name, long value) {
+    if (!name) return;
+    if (!strcmp(name, "strip_np")) cfg().strip_np = (int)value;
+    else if (!strcmp(name, "force_wide")) cfg().force_wide = (int)value;
+    else print_warning("unknown option %s", name);
+}
+
+size_t ssa_amd_search(p_query query, int algo, size_t hitcount, int bit_width, int mode, ssa_hit_t* out,
+                      size_t cap) {
+    test_configuration(query);
+    SearchResult R;
+    run_search(query, algo == SSA_AMD_NW ? kAlgoNW : kAlgoSW, hitcount, bit_width, mode == SSA_AMD_LOG, R);
+    const size_t n = std::min(cap, R.hits.size());
+    for (size_t i = 0; i < n; i++) {
+        const Hit& h = R.hits[i];
+        out[i] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
+    }
+    return n;
+}
+
+size_t ssa_amd_replay(const ssa_hit_t* log, size_t n, size_t hitcount, ssa_hit_t* out) {
+    TopK heap(hitcount);
+    for (size_t i = 0; i < n; i++) {
+        if (heap.full() && log[i].score <= heap.root_score()) continue;
+        heap.add(Hit{log[i].score, log[i].db_id, log[i].query_id, log[i].db_strand, log[i].db_frame});
+    }
+    std::vector<Hit> v = heap.sorted();
+    for (size_t i = 0; i < v.size(); i++)
+        out[i] = ssa_hit_t{v[i].score, v[i].id, v[i].qid, v[i].strand, v[i].frame, {0, 0, 0, 0, 0}};
+    return v.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+// common.h -- internal declarations shared by the libssa_amd host sources.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "libssa.h"
+#include "libssa_amd.h"
+#include "libssa_extern_db.h"
+
+namespace ssa {
+
+constexpr int kDim = 32;          // score matrix is 32 x 32, M(x,y) = m[(x << 5) + y]
+constexpr int kAlgoSW = 0;
+constexpr int kAlgoNW = 1;
+
+// ------------------------------------------------------------------ config
+struct Config {
+    int output_mode = OUTPUT_WARNING;     // reference util.c:34
+    size_t chunk_size = 1000;             // reference util.h:31 DEFAULT_CHUNK_SIZE
+    size_t thread_count = 0;              // 0 = all host cores
+    int symtype = AMINOACID;              // reference util_sequence.c:178
+    int strands = FORWARD_STRAND;         // util_sequence.c:179
+    int q_gencode = 1, d_gencode = 1;
+    int8_t gap_open = 0, gap_extend = 0;  // libssa.c:35-36
+    int device = -1;                      // -1: current HIP device
+    size_t id_offset = 0;                 // global ID of local record 0
+    uint64_t db_generation = 0;           // bumped by init_db
+    // tuning knobs (ssa_amd_set_option)
+    int strip_np = 16;                    // packed rows per strip (2*np query rows)
+    int waves_per_block = 4;
+    int force_wide = 0;                   // 1: score everything with the int64 kernel
+};
+Config& cfg();
+
+// --------------------------------------------------------------- messages
+// Same channels and prefixes as the reference (util.c:36-89): errors and
+// warnings and infos go to stdout gated by the output mode, fatal goes to
+// stderr and exits with status 1.
+[[noreturn]] void fatal(const char* fmt, ...);
+void print_info(const char* fmt, ...);
+void print_warning(const char* fmt, ...);
+void print_error(const char* fmt, ...);
+
+// --------------------------------------------------------------- alphabets
+extern const signed char* map_aa();   // 256-entry ASCII -> code, -1 unknown
+extern const signed char* map_nt();
+uint8_t nt_complement(uint8_t code);
+void revcompl(const uint8_t* in, size_t len, uint8_t* out);
+void init_translation(int q_gencode, int d_gencode);
+bool gencode_valid(int code);
+// translate mapped NT codes, strand 0 = forward, 1 = reverse complement
+std::vector<uint8_t> translate(bool db_side, const uint8_t* dna, size_t len, int strand, int frame);
+
+// ----------------------------------------------------------------- matrix
+struct Matrix {
+    bool ready = false;
+    bool constant = false;                // reference never clears this flag
+    int64_t m[kDim * kDim];
+};
+Matrix& matrix();
+void matrix_builtin(const char* name);
+void matrix_from_string(const char* text);
+void matrix_from_file(const char* path);
+void matrix_constant(int match, int mismatch);
+void matrix_free();
+
+// ------------------------------------------------------------------ query
+struct SeqBuf {
+    std::vector<uint8_t> seq;   // codes, plus a trailing 0 kept for C callers
+    size_t len() const { return seq.empty() ? 0 : seq.size() - 1; }
+};
+}  // namespace ssa
+
+struct _query {
+    ssa::SeqBuf nt[2];
+    ssa::SeqBuf aa[6];
+    std::string header;
+    int symtype;
+};
+
+namespace ssa {
+struct QueryView {                // one search "query buffer" (searcher.c:42-90)
+    const uint8_t* seq;
+    size_t len;
+    int strand, frame;
+    char* cseq;                   // pointer handed out in q_seq_t.seq
+};
+std::vector<QueryView> query_views(p_query q);
+
+// ---------------------------------------------------------------- top-k
+struct Hit {
+    int64_t score;
+    uint64_t id;
+    uint8_t qid, strand, frame;
+};
+// Reference min-heap (minheap.c:50-106) with exact tie behaviour.
+class TopK {
+public:
+    explicit TopK(size_t k) : k_(k) { a_.reserve(k); }
+    // returns true when the element entered the heap
+    bool add(const Hit& h);
+    size_t size() const { return a_.size(); }
+    bool full() const { return a_.size() >= k_; }
+    int64_t root_score() const { return a_.empty() ? INT64_MIN : a_[0].score; }
+    std::vector<Hit> sorted() const;
+private:
+    size_t k_;
+    std::vector<Hit> a_;
+};
+void sort_hits(std::vector<Hit>& v);   // score desc, id desc (util.h:12)
+
+}  // namespace ssa

@@ -1,0 +1,439 @@
+// engine.cpp -- packs the plugin's DB into the device layout once (cached
+// until init_db / a symbol-type change), then runs searches on one device.
+//
+// Replaces the reference's per-search chunk pipeline (db_adapter.c:212-239
+// re-fetches and re-maps every sequence on every search) and its per-thread
+// SIMD drivers (search_16.c:92-134, search_8.c:94-146).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+#include "engine.h"
+
+namespace ssa {
+
+ssa_amd_stats_t& stats() {
+    static ssa_amd_stats_t s;
+    return s;
+}
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+void check(hipError_t e, const char* what) {
+    if (e != hipSuccess) fatal("HIP error in %s: %s", what, hipGetErrorString(e));
+}
+
+DeviceDB& device_db() {
+    static DeviceDB d;
+    return d;
+}
+
+static void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+void DeviceDB::release() {
+    if (device >= 0) (void)hipSetDevice(device);
+    dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
+    dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
+    dfree(d_work);
+    if (h_scores) (void)hipHostFree(h_scores);
+    if (h_ovf) (void)hipHostFree(h_ovf);
+    if (h_wide) (void)hipHostFree(h_wide);
+    d_groups = nullptr; d_res = nullptr; d_rowbuf = nullptr; d_lane_len = nullptr; d_lane_out = nullptr;
+    d_scores = nullptr; d_ovf = nullptr; d_wide = nullptr; d_qpt = nullptr; d_query = nullptr;
+    d_matrix = nullptr; d_work = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
+    h_scores_cap = qpt_cap = query_cap = work_cap = 0;
+    generation = ~0ull;
+    meta = EntryMeta();
+    lane_out.clear();
+}
+
+constexpr size_t kOvfCap = 1 << 20;      // overflow list capacity per view
+
+// ------------------------------------------------------------ entry codes
+// Mapped residues of one entry, as db_adapter.c:47-110 builds them: NT codes
+// (reverse complement for strand 1), translated frames for TRANS_DB/BOTH,
+// amino-acid codes otherwise; unknown symbols become 0.
+static size_t map_record(const char* s, size_t n, const signed char* map, uint8_t* out) {
+    size_t unknown = 0;
+    for (size_t i = 0; i < n; i++) {
+        const signed char m = map[(unsigned char)s[i]];
+        if (m >= 0) out[i] = (uint8_t)m;
+        else { out[i] = 0; unknown++; }
+    }
+    return unknown;
+}
+
+std::vector<uint8_t> fetch_entry_codes(uint64_t local_id, int strand, int frame) {
+    p_seqinfo si = ssa_db_get_sequence(local_id);
+    if (!si) fatal("Could not get sequence from DB: %ld", (long)local_id);
+    const int st = cfg().symtype;
+    std::vector<uint8_t> v(si->seqlen + 1, 0);
+    if (st == NUCLEOTIDE) {
+        map_record(si->seq, si->seqlen, map_nt(), v.data());
+        (void)strand;  // reference aligner.c:76 / util_sequence.c:394-402 never flips it here
+    } else if (st == TRANS_DB || st == TRANS_BOTH) {
+        map_record(si->seq, si->seqlen, map_nt(), v.data());
+        return translate(true, v.data(), si->seqlen, strand, frame);
+    } else {
+        map_record(si->seq, si->seqlen, map_aa(), v.data());
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------- packing
+namespace {
+struct Staged {
+    EntryMeta meta;
+    std::vector<uint64_t> off;       // entry -> offset into codes
+    std::vector<uint8_t> codes;
+};
+
+void stage_from_plugin(Staged& S) {
+    const int st = cfg().symtype, strands = cfg().strands;
+    const size_t count = ssa_db_get_sequence_count();
+    EntryMeta& M = S.meta;
+    M.records = count;
+    std::vector<uint8_t> nt;
+    for (size_t id = 0; id < count; id++) {
+        p_seqinfo si = ssa_db_get_sequence(id);
+        if (!si) break;
+        if (si->seqlen == 0) continue;
+        const size_t n = si->seqlen;
+        auto add = [&](const uint8_t* c, size_t len, int strand, int frame) {
+            M.id.push_back(id);
+            M.strand.push_back((uint8_t)strand);
+            M.frame.push_back((uint8_t)frame);
+            M.len.push_back((uint32_t)len);
+            S.off.push_back(S.codes.size());
+            S.codes.insert(S.codes.end(), c, c + len);
+            M.residues += len;
+        };
+        size_t unknown;
+        if (st == NUCLEOTIDE) {
+            nt.resize(n);
+            unknown = map_record(si->seq, n, map_nt(), nt.data());
+            add(nt.data(), n, 0, 0);
+            if (strands & 2) {
+                std::vector<uint8_t> rc(n);
+                revcompl(nt.data(), n, rc.data());
+                add(rc.data(), n, 1, 0);
+            }
+        } else if (st == TRANS_DB || st == TRANS_BOTH) {
+            nt.resize(n);
+            unknown = map_record(si->seq, n, map_nt(), nt.data());
+            if (strands == BOTH_STRANDS) {
+                for (int s = 0; s < 2; s++)
+                    for (int f = 0; f < 3; f++) {
+                        auto p = translate(true, nt.data(), n, s, f);
+                        add(p.data(), p.size() - 1, s, f);
+                    }
+            } else {
+                // reference quirk (db_adapter.c:85-93): strand field = strands
+                for (int f = 0; f < 3; f++) {
+                    auto p = translate(true, nt.data(), n, strands - 1, f);
+                    add(p.data(), p.size() - 1, strands, f);
+                }
+            }
+        } else {
+            const size_t base = S.codes.size();
+            S.codes.resize(base + n);
+            unknown = map_record(si->seq, n, map_aa(), S.codes.data() + base);
+            M.id.push_back(id);
+            M.strand.push_back(0);
+            M.frame.push_back(0);
+            M.len.push_back((uint32_t)n);
+            S.off.push_back(base);
+            M.residues += n;
+        }
+        if (unknown > 0) print_warning("%ld unknown symbols found and set to zero", (long)unknown);
+    }
+}
+}  // namespace
+
+void ensure_device_db() {
+    DeviceDB& D = device_db();
+    const Config& C = cfg();
+    int dev = C.device;
+    if (dev < 0) check(hipGetDevice(&dev), "hipGetDevice");
+    if (D.generation == C.db_generation && D.device == dev && D.symtype == C.symtype &&
+        D.strands == C.strands && D.dgencode == C.d_gencode)
+        return;
+    const double t0 = now_ms();
+    D.release();
+    check(hipSetDevice(dev), "hipSetDevice");
+    D.device = dev;
+    if (!D.stream) {
+        check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
+    }
+
+    Staged S;
+    stage_from_plugin(S);
+    const size_t E = S.meta.size();
+
+    // length-sorted groups of 64 lanes (longest first: long waves start early)
+    std::vector<uint32_t> order(E);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return S.meta.len[a] > S.meta.len[b]; });
+    const uint32_t ngroups = (uint32_t)((E + 63) / 64);
+    std::vector<GroupDesc> groups(ngroups);
+    uint64_t blocks = 0;
+    for (uint32_t g = 0; g < ngroups; g++) {
+        const uint32_t longest = S.meta.len[order[(size_t)g * 64]];
+        const uint32_t ncols = ((longest + 1) + 15) / 16 * 16;
+        groups[g].blk = (uint32_t)blocks;
+        groups[g].ncols = ncols;
+        blocks += ncols / 16;
+    }
+    if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
+    std::vector<uint32_t> lane_len((size_t)ngroups * 64, 0), lane_out((size_t)ngroups * 64, 0xffffffffu);
+    std::vector<uint8_t> res((size_t)blocks * 1024, kPadCode);
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nth; t++) {
+        pool.emplace_back([&, t]() {
+            for (uint32_t g = t; g < ngroups; g += nth) {
+                uint8_t* gbase = res.data() + (size_t)groups[g].blk * 1024;
+                for (uint32_t l = 0; l < 64; l++) {
+                    const size_t pos = (size_t)g * 64 + l;
+                    if (pos >= E) break;
+                    const uint32_t e = order[pos];
+                    const uint32_t n = S.meta.len[e];
+                    lane_len[pos] = n;
+                    lane_out[pos] = e;
+                    const uint8_t* src = S.codes.data() + S.off[e];
+                    for (uint32_t c = 0; c < n; c += 16)
+                        std::memcpy(gbase + (size_t)(c / 16) * 1024 + l * 16, src + c, std::min(16u, n - c));
+                }
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+
+    // upload
+    auto dalloc = [&](void** p, size_t bytes, const char* what) {
+        check(hipMalloc(p, bytes ? bytes : 16), what);
+    };
+    dalloc((void**)&D.d_groups, groups.size() * sizeof(GroupDesc), "groups");
+    dalloc((void**)&D.d_res, res.size(), "residues");
+    dalloc((void**)&D.d_rowbuf, res.size() * 4, "row buffer");
+    dalloc((void**)&D.d_lane_len, lane_len.size() * 4, "lane_len");
+    dalloc((void**)&D.d_lane_out, lane_out.size() * 4, "lane_out");
+    dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
+    dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
+    dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
+    dalloc((void**)&D.d_matrix, 1024 * 8, "matrix");
+    check(hipHostMalloc((void**)&D.h_ovf, (kOvfCap + 1) * 4, hipHostMallocDefault), "pinned");
+    check(hipHostMalloc((void**)&D.h_wide, kOvfCap * 8, hipHostMallocDefault), "pinned");
+    check(hipMemcpy(D.d_groups, groups.data(), groups.size() * sizeof(GroupDesc), hipMemcpyHostToDevice), "H2D");
+    check(hipMemcpy(D.d_res, res.data(), res.size(), hipMemcpyHostToDevice), "H2D residues");
+    check(hipMemcpy(D.d_lane_len, lane_len.data(), lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
+    check(hipMemcpy(D.d_lane_out, lane_out.data(), lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
+    D.ngroups = ngroups;
+    D.nblocks = blocks;
+    D.meta = std::move(S.meta);
+    D.lane_out = std::move(lane_out);
+    D.generation = C.db_generation;
+    D.symtype = C.symtype;
+    D.strands = C.strands;
+    D.dgencode = C.d_gencode;
+    stats().pack_ms = now_ms() - t0;
+}
+
+// ----------------------------------------------------------------- search
+// Largest DB entry length n for which int16 NW provably never saturates:
+// every H is bounded below by the two-gap path 2Q+(i+j+2)R and above by
+// min(m,n)*maxM, and E/F/diagonal intermediates stay within one extra gap or
+// score of those bounds.
+static uint32_t nw_int16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM) {
+    if (Q > 0 || R > 0) return 0;
+    const int64_t up = std::max<int64_t>(maxM, 0), lo = std::min<int64_t>(minM, 0);
+    auto ok = [&](uint64_t n) {
+        const int64_t U = (int64_t)std::min<uint64_t>(m, n) * up + up;
+        const int64_t L = 3 * (int64_t)Q + (int64_t)(m + n + 4) * R + lo;
+        return U <= 32766 && L >= -32767;
+    };
+    if (!ok(0)) return 0;
+    uint64_t a = 0, b = 0xffffffffull;
+    if (ok(b)) return 0xffffffffu;
+    while (b - a > 1) {
+        const uint64_t c = (a + b) / 2;
+        if (ok(c)) a = c; else b = c;
+    }
+    return (uint32_t)a;
+}
+
+void device_search(const std::vector<QueryView>& views, int algo, SearchScores& out) {
+    DeviceDB& D = device_db();
+    check(hipSetDevice(D.device), "hipSetDevice");
+    const Config& C = cfg();
+    const size_t E = D.meta.size();
+    const size_t V = views.size();
+    const int np = (C.strip_np == 8 || C.strip_np == 32) ? C.strip_np : 16;
+    const bool nw = algo == kAlgoNW;
+    const int Q = C.gap_open, R = C.gap_extend;
+    const int64_t* M = matrix().m;
+
+    if (D.h_scores_cap < V * E) {
+        if (D.h_scores) (void)hipHostFree(D.h_scores);
+        check(hipHostMalloc((void**)&D.h_scores, std::max<size_t>(V * E, 1) * 4, hipHostMallocDefault), "pinned scores");
+        D.h_scores_cap = V * E;
+    }
+    out.s32 = D.h_scores;
+    out.entries = E;
+    out.views = V;
+    out.wide.clear();
+    out.cells = 0;
+    float kms = 0, wms = 0, dms = 0;
+    uint64_t wide_total = 0;
+    uint64_t kernel_bytes = 0;
+
+    for (size_t v = 0; v < V; v++) {
+        const QueryView& qv = views[v];
+        const size_t m = qv.len;
+        out.cells += (uint64_t)m * D.meta.residues;
+        int32_t* hs = D.h_scores + v * E;
+        if (E == 0) continue;
+        if (m == 0) {
+            // no query rows: SW scores 0, NW the boundary value H(-1, n-1)
+            for (size_t e = 0; e < E; e++)
+                hs[e] = nw ? (int32_t)(Q + (int64_t)D.meta.len[e] * R) : 0;
+            continue;
+        }
+        // profile bounds over every residue code a DB entry can hold
+        int64_t minM = INT64_MAX, maxM = INT64_MIN;
+        for (size_t i = 0; i < m; i++)
+            for (int c = 0; c < 31; c++) {
+                const int64_t x = M[(c << 5) + qv.seq[i]];
+                minM = std::min(minM, x);
+                maxM = std::max(maxM, x);
+            }
+        const bool fits16 = minM >= -32768 && maxM <= 32767;
+        uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(m, Q, R, minM, maxM) : 0xffffffffu) : 0;
+        if (C.force_wide) nmax16 = 0;
+
+        // strip profile table: dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r])
+        const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
+        std::vector<uint32_t> qpt((size_t)nstrips * 32 * np);
+        const int16_t padv = nw ? 0 : -32768;
+        auto val = [&](int c, size_t i) -> int16_t {
+            if (c == kPadCode || i >= m) return padv;
+            const int64_t x = M[(c << 5) + qv.seq[i]];
+            return (int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, x));
+        };
+        for (uint32_t s = 0; s < nstrips; s++)
+            for (int c = 0; c < 32; c++)
+                for (int r = 0; r < np; r++) {
+                    const size_t i = (size_t)s * 2 * np + r;
+                    qpt[((size_t)s * 32 + c) * np + r] =
+                        (uint32_t)(uint16_t)val(c, i) | ((uint32_t)(uint16_t)val(c, i + np) << 16);
+                }
+        if (D.qpt_cap < qpt.size()) {
+            dfree(D.d_qpt);
+            check(hipMalloc((void**)&D.d_qpt, qpt.size() * 4), "qpt");
+            D.qpt_cap = qpt.size();
+        }
+        if (D.query_cap < m) {
+            dfree(D.d_query);
+            check(hipMalloc((void**)&D.d_query, m), "query");
+            D.query_cap = m;
+        }
+        const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
+        if (D.work_cap < (size_t)wide_threads * 2 * m) {
+            dfree(D.d_work);
+            check(hipMalloc((void**)&D.d_work, (size_t)wide_threads * 2 * m * 8), "wide scratch");
+            D.work_cap = (size_t)wide_threads * 2 * m;
+        }
+        hipStream_t st = D.stream;
+        check(hipMemcpyAsync(D.d_qpt, qpt.data(), qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+        check(hipMemcpyAsync(D.d_query, qv.seq, m, hipMemcpyHostToDevice, st), "H2D query");
+        check(hipMemcpyAsync(D.d_matrix, M, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
+
+        StripArgs a{};
+        a.res = D.d_res;
+        a.rowbuf = D.d_rowbuf;
+        a.groups = D.d_groups;
+        a.lane_len = D.d_lane_len;
+        a.lane_out = D.d_lane_out;
+        a.qpt = D.d_qpt;
+        a.scores = D.d_scores;
+        a.ovf_list = D.d_ovf + 1;
+        a.ovf_count = D.d_ovf;
+        a.ngroups = D.ngroups;
+        a.nstrips = nstrips;
+        a.m = (uint32_t)m;
+        a.gap_open = Q;
+        a.gap_extend = R;
+        a.nmax16 = nmax16;
+        a.ovf_cap = (uint32_t)kOvfCap;
+
+        WideArgs w{};
+        w.res = D.d_res;
+        w.groups = D.d_groups;
+        w.lane_len = D.d_lane_len;
+        w.ovf_list = D.d_ovf + 1;
+        w.ovf_count = D.d_ovf;
+        w.query = D.d_query;
+        w.matrix = D.d_matrix;
+        w.work = D.d_work;
+        w.wide_scores = D.d_wide;
+        w.m = (uint32_t)m;
+        w.gap_open = Q;
+        w.gap_extend = R;
+        w.nw = nw ? 1 : 0;
+        w.ovf_cap = (uint32_t)kOvfCap;
+
+        check(hipEventRecord(D.ev[0], st), "event");
+        check(launch_strip16(a, np, nw, st), "strip16 kernel launch");
+        check(hipEventRecord(D.ev[1], st), "event");
+        check(launch_wide(w, wide_threads, st), "wide kernel launch");
+        check(hipEventRecord(D.ev[2], st), "event");
+        check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
+        check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
+        check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
+        check(hipEventRecord(D.ev[3], st), "event");
+        check(hipStreamSynchronize(st), "search");
+        uint32_t nov = D.h_ovf[0];
+        if (nov > kOvfCap) fatal("overflow list exhausted (%u entries)", nov);
+        if (nov > 4096) {
+            check(hipMemcpy(D.h_ovf, D.d_ovf, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
+            check(hipMemcpy(D.h_wide, D.d_wide, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
+        }
+        for (uint32_t i = 0; i < nov; i++) {
+            const uint32_t e = D.lane_out[D.h_ovf[1 + i]];
+            out.wide[(uint64_t)v * E + e] = D.h_wide[i];
+        }
+        wide_total += nov;
+        float t;
+        check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
+        kms += t;
+        check(hipEventElapsedTime(&t, D.ev[1], D.ev[2]), "elapsed");
+        wms += t;
+        check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
+        dms += t;
+        // algorithmic bytes: residues once + per-entry score write + profile
+        kernel_bytes += D.meta.residues + 4ull * E + qpt.size() * 4;
+    }
+    ssa_amd_stats_t& S = stats();
+    S.kernel_ms = kms;
+    S.wide_ms = wms;
+    S.d2h_ms = dms;
+    S.cells = out.cells;
+    S.entries = E;
+    S.wide_count = wide_total;
+    S.kernel_launches = (uint32_t)V;
+    S.device = D.device;
+    S.kernel_bytes = kernel_bytes;
+}
+
+}  // namespace ssa

@@ -1,0 +1,82 @@
+// engine.h -- device-resident packed DB and the per-device search.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+
+// One DB "entry" = one scored sequence: a non-empty DB record, or one of its
+// strands (NUCLEOTIDE with the complementary strand) -- the reference's
+// sdb_sequence_t (libssa_datatypes.h:88-96, db_adapter.c:47-110).
+struct EntryMeta {
+    std::vector<uint64_t> id;       // local record ID per entry (ascending)
+    std::vector<uint8_t> strand;
+    std::vector<uint8_t> frame;
+    std::vector<uint32_t> len;
+    uint64_t residues = 0;
+    size_t records = 0;             // IDs the plugin handed out
+    size_t size() const { return id.size(); }
+};
+
+struct DeviceDB {
+    int device = -1;
+    uint64_t generation = ~0ull;
+    int symtype = -1, strands = -1, dgencode = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    EntryMeta meta;
+    uint32_t ngroups = 0;
+    uint64_t nblocks = 0;                 // 1 KiB residue blocks
+    GroupDesc* d_groups = nullptr;
+    uint4* d_res = nullptr;
+    uint4* d_rowbuf = nullptr;
+    uint32_t* d_lane_len = nullptr;
+    uint32_t* d_lane_out = nullptr;
+    int32_t* d_scores = nullptr;
+    int32_t* h_scores = nullptr;          // pinned, [views][entries]
+    size_t h_scores_cap = 0;
+    uint32_t* d_ovf = nullptr;            // [0] = count, [1..] = list
+    uint32_t* h_ovf = nullptr;            // pinned
+    int64_t* d_wide = nullptr;
+    int64_t* h_wide = nullptr;            // pinned
+    uint32_t* d_qpt = nullptr;
+    size_t qpt_cap = 0;
+    uint8_t* d_query = nullptr;
+    size_t query_cap = 0;
+    int64_t* d_matrix = nullptr;
+    int64_t* d_work = nullptr;
+    size_t work_cap = 0;
+    std::vector<uint32_t> lane_out;       // host copy for overflow mapping
+    void release();
+};
+DeviceDB& device_db();
+void ensure_device_db();                  // (re)packs from the plugin when stale
+std::vector<uint8_t> fetch_entry_codes(uint64_t local_id, int strand, int frame);
+
+// Exact scores of every entry for every query view.  Scores live in the
+// pinned int32 buffer (view-major); entries re-scored by the int64 kernel
+// read INT32_MIN there and have their value in `wide`.
+struct SearchScores {
+    const int32_t* s32 = nullptr;
+    size_t entries = 0, views = 0;
+    std::unordered_map<uint64_t, int64_t> wide;   // key = view * entries + entry
+    uint64_t cells = 0;
+    int64_t get(size_t v, size_t e) const {
+        const int32_t x = s32[v * entries + e];
+        if (x != INT32_MIN) return x;
+        auto it = wide.find((uint64_t)v * entries + e);
+        return it == wide.end() ? (int64_t)INT32_MIN : it->second;
+    }
+};
+void device_search(const std::vector<QueryView>& views, int algo, SearchScores& out);
+
+ssa_amd_stats_t& stats();
+void check(hipError_t e, const char* what);
+double now_ms();
+
+}  // namespace ssa

@@ -1,0 +1,51 @@
+// kernels.h -- argument blocks of the HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ssa {
+
+constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
+constexpr uint8_t kPadCode = 31;   // residue code of padding columns (never a real residue)
+
+struct GroupDesc {
+    uint32_t blk;     // residue offset in 1 KiB blocks (16 columns x 64 lanes)
+    uint32_t ncols;   // padded column count, multiple of 16, >= longest + 1
+};
+
+struct StripArgs {
+    const uint4* res;          // packed residues
+    uint4* rowbuf;             // strip boundary buffer (4 B per lane and column)
+    const GroupDesc* groups;
+    const uint32_t* lane_len;  // [ngroups * 64]
+    const uint32_t* lane_out;  // [ngroups * 64] dense output index
+    const uint32_t* qpt;       // [nstrips][32][np] packed query profile
+    int32_t* scores;           // [entries]
+    uint32_t* ovf_list;        // lanes that need the exact int64 re-score
+    uint32_t* ovf_count;
+    uint32_t ngroups, nstrips, m;
+    int32_t gap_open, gap_extend;
+    uint32_t nmax16;           // longest DB entry proven int16-safe
+    uint32_t ovf_cap;          // capacity of ovf_list
+};
+
+struct WideArgs {
+    const uint4* res;
+    const GroupDesc* groups;
+    const uint32_t* lane_len;
+    const uint32_t* ovf_list;
+    const uint32_t* ovf_count;
+    const uint8_t* query;      // [m]
+    const int64_t* matrix;     // [1024]
+    int64_t* work;             // [threads][2m]
+    int64_t* wide_scores;      // [ovf_count]
+    uint32_t m;
+    int32_t gap_open, gap_extend;
+    int32_t nw;
+    uint32_t ovf_cap;
+};
+
+hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
+hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
+
+}  // namespace ssa

@@ -1,0 +1,355 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the database-search hot path.
+//
+// Replaces the reference's inter-sequence SIMD DP (src/algo/simd/
+// search_simd_sw.c:172-441 and search_simd_nw.c:180-516) and its 64-bit
+// fallback (src/algo/64/smith_waterman_63.c:32-98,
+// needleman_wunsch_64.c:32-98).  Design:
+//
+//  * one wavefront = one "group" of 64 length-sorted DB sequences, one
+//    sequence per lane.  The DP is swept in horizontal strips of 2*NP query
+//    rows; inside a strip every lane keeps its H and E state for the strip's
+//    rows in VGPRs as packed int16 pairs and walks its sequence column by
+//    column.
+//  * packing: the low half of each 32-bit register holds strip row r at
+//    column j, the high half holds row r+NP at column j-1 (a one-column skew),
+//    so one v_pk_add_i16 / v_pk_max_i16 advances two cells of the same
+//    sequence and the vertical (F) dependency between the halves is carried
+//    from one step to the next.
+//  * the strip's query profile QP[db symbol][row] lives in LDS (one table per
+//    wave); each step a lane reads the NP-dword row of its current residue;
+//    the high halves come from the previous residue's row (kept in VGPRs).
+//  * saturating signed int16 arithmetic (v_pk_add_i16 ... clamp).  SW uses
+//    the biased encoding value-32768 so the local-alignment floor at 0 is the
+//    saturation floor; NW is unbiased.  A lane whose SW maximum saturates, or
+//    whose NW length exceeds the host-proven int16-safe bound, is appended
+//    to an overflow list and re-scored exactly by wide_kernel (int64).
+//  * strip boundaries (H and F of the strip's last row per column) go to a
+//    per-lane row buffer in HBM, 4 bytes per column, coalesced 16 B per lane.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace ssa {
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+
+#define AS_U32(x) __builtin_bit_cast(uint32_t, (x))
+#define AS_S2(x) __builtin_bit_cast(s2, (uint32_t)(x))
+
+__device__ __forceinline__ s2 adds(s2 a, s2 b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ s2 vmax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ uint32_t perm(uint32_t hi_src, uint32_t lo_src, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi_src, lo_src, sel);
+}
+__device__ __forceinline__ short sat16(int v) { return (short)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+__device__ __forceinline__ uint32_t pack16(short lo, short hi) {
+    return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+}
+
+// byte selectors for v_perm_b32(a, b, sel): bytes 0-3 of b, 4-7 of a
+constexpr uint32_t SEL_LO_BHI_HI_ALO = 0x05040302u;  // lo = b.hi,  hi = a.lo
+constexpr uint32_t SEL_LO_BLO_HI_ALO = 0x05040100u;  // lo = b.lo,  hi = a.lo
+constexpr uint32_t SEL_LO_BHI_HI_AHI = 0x07060302u;  // lo = b.hi,  hi = a.hi
+
+template <int NP>
+__device__ __forceinline__ void load_row(uint32_t (&dst)[NP], const uint32_t* row) {
+#pragma unroll
+    for (int i = 0; i < NP / 4; i++) {
+        const uint4 v = *(const uint4*)(row + 4 * i);
+        dst[4 * i + 0] = v.x;
+        dst[4 * i + 1] = v.y;
+        dst[4 * i + 2] = v.z;
+        dst[4 * i + 3] = v.w;
+    }
+}
+
+template <int NP, bool NW>
+__global__ void __launch_bounds__(64 * kWaves)
+strip16_kernel(const StripArgs a) {
+    constexpr int ROWW = NP + 4;                  // padded LDS row (dwords), 16 B aligned
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[kWaves][32 * ROWW];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t g = blockIdx.x * kWaves + wave;
+    if (g >= a.ngroups) return;
+
+    uint32_t* lds = lds_all[wave];
+    const GroupDesc gd = a.groups[g];
+    const uint32_t nblk = gd.ncols >> 4;
+    const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
+    uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
+    const uint32_t gl = g * 64 + lane;
+    const uint32_t len = a.lane_len[gl];
+
+    const short Q = (short)a.gap_open, R = (short)a.gap_extend;
+    const s2 vQR = {(short)(Q + R), (short)(Q + R)};
+    const s2 vR = {R, R};
+    const short FLOOR = NW ? (short)0 : (short)-32768;  // SW biased zero
+    (void)FLOOR;
+
+    s2 S = {-32768, -32768};
+    s2 cap = {0, 0};
+    const int R2 = 2 * NP;
+    const int last_strip = (int)a.nstrips - 1;
+    const int rr = (int)a.m - 1 - last_strip * R2;     // strip row of the last query row
+    const int cap_half = rr >= NP ? 1 : 0;
+    const int cap_row = rr - cap_half * NP;
+    const uint32_t cap_col = len - 1 + cap_half;
+
+    for (int s = 0; s < (int)a.nstrips; s++) {
+        // ---- stage this strip's profile table into the wave's LDS table
+        const uint32_t* src = a.qpt + (size_t)s * 32 * NP;
+#pragma unroll
+        for (int i = 0; i < (32 * NP) / 64; i++) {
+            const int idx = i * 64 + lane;
+            lds[(idx / NP) * ROWW + (idx % NP)] = src[idx];
+        }
+        // one wave owns the table: its LDS ops complete in order, so a
+        // drained lgkmcnt plus a compiler barrier is the whole hand-off
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+        const bool first = (s == 0);
+        const bool capture = NW && (s == last_strip);
+        const int i0 = s * R2;     // first query row of the strip
+
+        // ---- left boundary (column -1)
+        s2 H[NP], E[NP];
+        uint32_t prevw[NP];
+#pragma unroll
+        for (int r = 0; r < NP; r++) {
+            if (NW) {
+                const int i = i0 + r;
+                H[r] = AS_S2(pack16(sat16(Q + (i + 1) * R), 0));
+                E[r] = AS_S2(pack16(sat16(2 * Q + (i + 2) * R), 0));
+            } else {
+                H[r] = AS_S2(0x80008000u);
+                E[r] = AS_S2(0x80008000u);
+            }
+            prevw[r] = 0x80008000u;     // row of the (virtual) residue before column 0
+        }
+        // diagonal input of the strip's first row at column 0: H(i0-1, -1)
+        s2 hd0 = NW ? AS_S2(pack16(first ? 0 : sat16(Q + i0 * R), 0)) : AS_S2(0x80008000u);
+        s2 Fprev = AS_S2(0x80008000u);
+        // synthesized top boundary for the first strip: (H(-1,j), F into row 0)
+        s2 rbsyn = NW ? AS_S2(pack16(sat16(Q + R), sat16(2 * Q + 2 * R))) : AS_S2(0x80008000u);
+
+        uint32_t ob[4] = {0, 0, 0, 0};
+        uint4 rnext = resp[0];
+        uint4 qnext = first ? make_uint4(0, 0, 0, 0) : rbp[0];
+        // profile row of the first residue, fetched ahead like every later one
+        uint32_t nxt[NP];
+        load_row<NP>(nxt, lds + (rnext.x & 0xffu) * ROWW);
+
+        for (uint32_t b = 0; b < nblk; b++) {
+            const uint4 rcur = rnext;
+            if (b + 1 < nblk) rnext = resp[(size_t)(b + 1) * 64];
+            const uint32_t rw[4] = {rcur.x, rcur.y, rcur.z, rcur.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint4 qcur = qnext;
+                if (!first) {
+                    const uint32_t nq = b * 4 + t + 1;
+                    if (nq < nblk * 4) qnext = rbp[(size_t)nq * 64];
+                }
+                const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = t * 4 + u;            // column within the block
+                    const uint32_t j = b * 16 + k;      // column of the low half
+                    uint32_t cur[NP];
+#pragma unroll
+                    for (int r = 0; r < NP; r++) cur[r] = nxt[r];
+                    // fetch the profile row of the next column's residue now,
+                    // so its LDS latency hides under this column's arithmetic
+                    {
+                        const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
+                                                   : (rnext.x & 0xffu);
+                        load_row<NP>(nxt, lds + dn * ROWW);
+                    }
+                    uint32_t rbv;
+                    if (first) {
+                        rbv = AS_U32(rbsyn);
+                        if (NW) rbsyn = adds(rbsyn, vR);
+                    } else {
+                        rbv = qw[u];
+                    }
+                    // F entering the first row of each half
+                    s2 F = AS_S2(perm(AS_U32(Fprev), rbv, SEL_LO_BHI_HI_ALO));
+                    s2 hd = hd0;
+#pragma unroll
+                    for (int r = 0; r < NP; r++) {
+                        const s2 P = AS_S2((cur[r] & 0xffffu) | (prevw[r] & 0xffff0000u));
+                        s2 h = adds(hd, P);
+                        h = vmax(h, E[r]);
+                        h = vmax(h, F);
+                        if (!NW) S = vmax(S, h);
+                        hd = H[r];
+                        H[r] = h;
+                        const s2 tt = adds(h, vQR);
+                        E[r] = vmax(adds(E[r], vR), tt);
+                        F = vmax(adds(F, vR), tt);
+                        prevw[r] = cur[r];
+                    }
+                    // hd = H[NP-1] before this step; next step's row-0 diagonals:
+                    // lo = H(i0-1, j) from the row buffer, hi = H(i0+NP-1, j-1)
+                    hd0 = AS_S2(perm(AS_U32(hd), rbv, SEL_LO_BLO_HI_ALO));
+                    Fprev = F;
+                    // materialize the running maximum every column; otherwise the
+                    // compiler defers the max chain and keeps every H alive
+                    if (!NW) asm volatile("" : "+v"(S));
+                    if (b == 0 && k == 0) {
+                        // the high half just processed the virtual column -1:
+                        // install the true left boundary for its rows
+                        if (NW) {
+#pragma unroll
+                            for (int r = 0; r < NP; r++) {
+                                const int i = i0 + NP + r;
+                                H[r] = AS_S2((AS_U32(H[r]) & 0xffffu) | ((uint32_t)(uint16_t)sat16(Q + (i + 1) * R) << 16));
+                                E[r] = AS_S2((AS_U32(E[r]) & 0xffffu) | ((uint32_t)(uint16_t)sat16(2 * Q + (i + 2) * R) << 16));
+                            }
+                        }
+                    } else {
+                        // bottom boundary of column j-1 (high half): (H, F) of row i0+2NP-1
+                        ob[(k + 3) & 3] = perm(AS_U32(F), AS_U32(H[NP - 1]), SEL_LO_BHI_HI_AHI);
+                        if ((k & 3) == 0)
+                            rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                    }
+                    if (capture) {
+                        s2 hsel = H[0];
+#pragma unroll
+                        for (int r = 1; r < NP; r++) hsel = (cap_row == r) ? H[r] : hsel;
+                        cap = (j == cap_col) ? hsel : cap;
+                    }
+                    // keep the scheduler from hoisting later columns' LDS reads
+                    // (register pressure): one column in flight at a time
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        // the last column of the strip is never produced (the high half lags);
+        // store a neutral boundary so the next strip reads defined values
+        ob[3] = NW ? 0x80008000u : 0x80008000u;
+        rbp[(size_t)(nblk * 4 - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // table reads done before restaging
+    }
+
+    const uint32_t o = a.lane_out[gl];
+    if (o == 0xffffffffu) return;            // padding lane of the last group
+    if (len == 0) {                          // empty translated frame: full_sw 0, full_nw H(m-1,-1)
+        a.scores[o] = NW ? (int32_t)(a.gap_open + (int64_t)a.m * a.gap_extend) : 0;
+        return;
+    }
+    int32_t score;
+    bool ovf = len > a.nmax16;
+    if (!NW) {
+        const short smax = S.x > S.y ? S.x : S.y;
+        ovf = ovf || smax == 32767;
+        score = (int32_t)smax + 32768;
+    } else {
+        score = cap_half ? cap.y : cap.x;
+    }
+    if (ovf) {
+        const uint32_t idx = atomicAdd(a.ovf_count, 1u);
+        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;   // host aborts when the count exceeds the cap
+        a.scores[o] = INT32_MIN;
+    } else {
+        a.scores[o] = score;
+    }
+}
+
+// Exact int64 re-score of overflowed lanes: the reference's 64-bit
+// recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
+__global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
+    const uint32_t n = min(*a.ovf_count, a.ovf_cap);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    int64_t* he = a.work + (size_t)tid * 2 * (a.m ? a.m : 1);
+    const int64_t Q = a.gap_open, R = a.gap_extend;
+    for (uint32_t i = tid; i < n; i += stride) {
+        const uint32_t gl = a.ovf_list[i];
+        const uint32_t g = gl >> 6, lane = gl & 63;
+        const uint32_t len = a.lane_len[gl];
+        const uint8_t* base = (const uint8_t*)a.res + (size_t)a.groups[g].blk * 1024 + lane * 16;
+        int64_t score;
+        if (!a.nw) {
+            int64_t smax = 0;
+            for (uint32_t q = 0; q < a.m; q++) { he[2 * q] = 0; he[2 * q + 1] = 0; }
+            for (uint32_t j = 0; j < len; j++) {
+                const uint32_t d = base[(size_t)(j >> 4) * 1024 + (j & 15)];
+                const int64_t* mrow = a.matrix + (d << 5);
+                int64_t h = 0, f = 0;
+                for (uint32_t q = 0; q < a.m; q++) {
+                    const int64_t nd = he[2 * q];
+                    int64_t e = he[2 * q + 1];
+                    h += mrow[a.query[q]];
+                    if (e > h) h = e;
+                    if (f > h) h = f;
+                    if (h < 0) h = 0;
+                    if (h > smax) smax = h;
+                    he[2 * q] = h;
+                    e += R;
+                    f += R;
+                    h += Q + R;
+                    if (h > e) e = h;
+                    if (h > f) f = h;
+                    he[2 * q + 1] = e;
+                    h = nd;
+                }
+            }
+            score = smax;
+        } else {
+            for (uint32_t q = 0; q < a.m; q++) {
+                he[2 * q] = Q + (int64_t)(q + 1) * R;
+                he[2 * q + 1] = 2 * Q + (int64_t)(q + 2) * R;
+            }
+            for (uint32_t j = 0; j < len; j++) {
+                const uint32_t d = base[(size_t)(j >> 4) * 1024 + (j & 15)];
+                const int64_t* mrow = a.matrix + (d << 5);
+                int64_t f = 2 * Q + (int64_t)(j + 2) * R;
+                int64_t h = j == 0 ? 0 : Q + (int64_t)j * R;
+                for (uint32_t q = 0; q < a.m; q++) {
+                    const int64_t nd = he[2 * q];
+                    int64_t e = he[2 * q + 1];
+                    h += mrow[a.query[q]];
+                    if (f > h) h = f;
+                    if (e > h) h = e;
+                    he[2 * q] = h;
+                    e += R;
+                    f += R;
+                    h += Q + R;
+                    if (f < h) f = h;
+                    if (e < h) e = h;
+                    he[2 * q + 1] = e;
+                    h = nd;
+                }
+            }
+            score = a.m ? he[2 * a.m - 2] : 0;
+        }
+        a.wide_scores[i] = score;
+    }
+}
+
+// ------------------------------------------------------------------ launch
+template <int NP, bool NW>
+static hipError_t launch_np(const StripArgs& a, hipStream_t st) {
+    const uint32_t blocks = (a.ngroups + kWaves - 1) / kWaves;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((strip16_kernel<NP, NW>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st) {
+    if (np == 8) return nw ? launch_np<8, true>(a, st) : launch_np<8, false>(a, st);
+    if (np == 32) return nw ? launch_np<32, true>(a, st) : launch_np<32, false>(a, st);
+    return nw ? launch_np<16, true>(a, st) : launch_np<16, false>(a, st);
+}
+
+hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {
+    const uint32_t blocks = (threads + 63) / 64;
+    hipLaunchKernelGGL(wide_kernel, dim3(blocks), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace ssa

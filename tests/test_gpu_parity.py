@@ -1,0 +1,266 @@
+"""GPU parity: the HIP path through the C ABI against the oracle.
+
+Everything here calls libssa_amd.so (sw_align / nw_align / ssa_amd_search),
+which scores on the MI355X; the expected values come from the reference's own
+fixtures (tests/golden) or from the oracle (oracle/ssa_oracle.c) on the same
+seeded inputs.  Integer work: the bar is bit-exact scores AND the same IDs
+among equal scores as the reference's 64-bit single-thread run.
+"""
+import hashlib
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import libssa_amd as S
+from libssa_amd import synthetic as syn
+from oracle import pyoracle as po
+from tests.conftest import DATA, GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+KATS = json.load(open(os.path.join(GOLDEN, "kat.json")))
+TABLES = np.load(os.path.join(GOLDEN, "tables.npz"))
+NAMES = [str(x) for x in TABLES["names"]]
+
+
+def configure(nucleotide, spec, go, ge, chunk=1000, strands=S.FORWARD_STRAND):
+    S.set_output_mode(S.OUTPUT_ERROR)
+    S.init_symbol_translation(S.NUCLEOTIDE if nucleotide else S.AMINOACID, strands, 1, 1)
+    if spec[0] == "const":
+        S.init_constant_scores(spec[1], spec[2])
+    elif spec[0] == "builtin":
+        S.init_score_matrix(S.MATRIX_BUILDIN, spec[1])
+    else:
+        S.init_score_matrix(S.READ_FROM_FILE, os.path.join(DATA, spec[1]))
+    S.init_gap_penalties(go, ge)
+    S.set_chunk_size(chunk)
+
+
+def make_query(q):
+    if q.startswith("file:"):
+        return S.init_sequence_fasta(S.READ_FROM_FILE, os.path.join(DATA, q[5:]))
+    return S.init_sequence_fasta(S.READ_FROM_STRING, q[4:])
+
+
+# public-API runnable KATs (NUCLEOTIDE needs constant scoring, libssa.c:214-216)
+API_KATS = [c for c in KATS if not (c["nucleotide"] and c["scoring"][0] != "const")]
+
+
+@pytest.mark.parametrize("case", API_KATS, ids=[c["name"] for c in API_KATS])
+@pytest.mark.parametrize("width", [S.BIT_WIDTH_16, S.BIT_WIDTH_8, S.BIT_WIDTH_64])
+def test_kat_public_api(case, width):
+    configure(case["nucleotide"], case["scoring"], case["gap_open"], case["gap_extend"], case["chunk"])
+    S.init_db(os.path.join(DATA, case["db"]))
+    q = make_query(case["query"])
+    for algo, fn in (("sw", S.sw_align), ("nw", S.nw_align)):
+        got = [(h["score"], h["id"]) for h in fn(q, case["k"], width)]
+        assert got == [tuple(x) for x in case[algo + "_64"]], (algo, got[:5])
+    S.free_sequence(q)
+
+
+@pytest.mark.parametrize("np_", [8, 16, 32])
+def test_strip_heights_agree(np_):
+    case = next(c for c in KATS if c["name"] == "config1_Q3ZAI3_k300")
+    configure(False, case["scoring"], -11, -1)
+    S.init_db(os.path.join(DATA, case["db"]))
+    q = make_query(case["query"])
+    S.set_option("strip_np", np_)
+    try:
+        for algo, fn in (("sw", S.sw_align), ("nw", S.nw_align)):
+            got = [(h["score"], h["id"]) for h in fn(q, 300, 16)]
+            assert got == [tuple(x) for x in case[algo + "_64"]]
+    finally:
+        S.set_option("strip_np", 16)
+    S.free_sequence(q)
+
+
+def _write_db(tmp, codes, off, nucleotide=False):
+    path = os.path.join(tmp, "db.fas")
+    syn.write_fasta(path, codes, off, nucleotide)
+    return path
+
+
+def _full_scores(q, algo, n_entries):
+    """Every entry's exact score, via the insertion log with k >= #entries."""
+    log = S.search(q, algo, n_entries, 16, S.LOG, cap=n_entries + 8)
+    log.sort(key=lambda h: h[1])
+    return np.array([h[0] for h in log], dtype=np.int64), np.array([h[1] for h in log], dtype=np.uint64)
+
+
+@pytest.mark.parametrize("fname", sorted(f for f in os.listdir(GOLDEN) if f.startswith("random_")))
+def test_random_golden_full_score_vectors(fname):
+    z = np.load(os.path.join(GOLDEN, fname))
+    meta = json.loads(str(z["meta"]))
+    q = syn.protein_query(meta["qlen"], meta["qseed"])
+    codes, off = syn.protein_db(meta["n"], meta["seed"], query=q, plant_every=meta["plant_every"],
+                                lo=meta["lo"], hi=meta["hi"])
+    lens = np.diff(off)
+    keep = np.nonzero(lens > 0)[0]
+    configure(False, ("builtin", meta["matrix"]), meta["gap_open"], meta["gap_extend"])
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for algo, an in ((S.SW, "sw"), (S.NW, "nw")):
+            sc, ids = _full_scores(qq, algo, len(keep))
+            assert (ids == keep).all()
+            assert (sc == z[an + "_scores"][keep]).all(), np.nonzero(sc != z[an + "_scores"][keep])[0][:10]
+            for k in (1, 10, 100, 1000):
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                got = [(h["score"], h["id"]) for h in fn(qq, k, 16)]
+                assert got == [tuple(x) for x in meta[f"{an}_top{k}"]]
+        S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_query_length_edges_vs_oracle(qlen, algo):
+    rng = np.random.default_rng(qlen)
+    q = syn.protein_query(qlen, 100 + qlen)
+    # lengths straddling the 16-column blocks, plus empty records
+    lens = np.array([0, 1, 2, 3, 15, 16, 17, 31, 32, 33, 47, 48, 49, 64, 65, 200, 0, 511, 512, 513]
+                    + list(rng.integers(1, 300, 300)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for np_ in (8, 16, 32):
+            S.set_option("strip_np", np_)
+            sc, ids = _full_scores(qq, algo, len(keep))
+            assert (ids == keep).all()
+            assert (sc == exp).all(), (np_, np.nonzero(sc != exp)[0][:10])
+        S.set_option("strip_np", 16)
+        S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_wide_kernel_matches_oracle(algo):
+    """Every entry forced through the exact int64 re-score kernel."""
+    q = syn.protein_query(77, 5)
+    codes, off = syn.protein_db(700, 9, query=q, plant_every=100, lo=1, hi=400)
+    M = TABLES["matrices"][NAMES.index("blosum50")].copy()
+    exp = po.scores(algo, q, codes, off, M, -10, -2)
+    configure(False, ("builtin", "blosum50"), -10, -2)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        S.set_option("force_wide", 1)
+        try:
+            sc, _ = _full_scores(qq, algo, 700)
+        finally:
+            S.set_option("force_wide", 0)
+        assert (sc == exp).all()
+        assert S.stats()["wide_count"] == 700
+        S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_int16_overflow_reroute(algo):
+    """Scores beyond int16 (SW >= 65535, NW beyond the proven bound) come
+    back exact through the overflow list (reference test_searcher.c:507-536
+    shape: constant 127/-1 self-alignment)."""
+    rng = np.random.default_rng(3)
+    base = rng.choice(syn.AA_CODES, size=900).astype(np.uint8)
+    seqs = [base, base[:600], rng.choice(syn.AA_CODES, size=300).astype(np.uint8), base[100:]]
+    codes = np.concatenate(seqs)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    M = po.matrix_constant(127, -1)
+    exp = po.scores(algo, base, codes, off, M, -1, -1)
+    assert exp.max() > 65535
+    configure(False, ("const", 127, -1), -1, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(base))
+        sc, _ = _full_scores(qq, algo, 4)
+        assert (sc == exp).all()
+        assert S.stats()["wide_count"] >= 1
+        S.free_sequence(qq)
+
+
+def test_shard_logs_replay_to_global_result():
+    """The insertion logs of consecutive ID shards, concatenated in shard
+    order and replayed, equal the single-DB top-k including tie IDs."""
+    q = syn.protein_query(60, 1)
+    codes, off = syn.protein_db(4000, 2, query=q, plant_every=300, lo=10, hi=200)
+    n = 4000
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        qs = syn.query_string(q)
+        full = {}
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, qs)
+        for k in (1, 7, 50, 333):
+            full[k] = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+        cuts = [0, 1000, 1700, 3100, n]
+        for k in (1, 7, 50, 333):
+            log = []
+            for r in range(len(cuts) - 1):
+                a, b = cuts[r], cuts[r + 1]
+                sub_off = off[a:b + 1] - off[a]
+                path = os.path.join(tmp, f"shard{r}.fas")
+                syn.write_fasta(path, codes[int(off[a]):int(off[b])], sub_off)
+                S.init_db(path)
+                S.set_id_offset(a)
+                log += S.search(qq, S.SW, k, 16, S.LOG)
+            S.set_id_offset(0)
+            assert S.replay(log, k) == full[k]
+        S.free_sequence(qq)
+
+
+def test_nucleotide_both_strands_and_multi_query():
+    """NUCLEOTIDE with both strands: 2 query strands x 2 DB strands, heap
+    order chunk by chunk (search_64.c:44-56); checked against a CPU replay
+    of the same insertion order built from oracle scores."""
+    seqs = po.read_fasta(os.path.join(DATA, "AF091148.fas"))[:300]
+    dbc = [po.map_db(s, True) for s in seqs]
+    qraw = po.read_query_fasta(os.path.join(DATA, "one_seq.fas"))
+    qf = po.map_query(qraw, True)
+    comp = np.array([0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15], np.uint8)
+    qr = comp[qf[::-1]]
+    M = po.matrix_constant(2, -3)
+    entries = []
+    for i, d in enumerate(dbc):
+        if len(d):
+            entries.append((i, 0, d))
+            entries.append((i, 1, comp[d[::-1]]))
+    db, off = po.pack_db([e[2] for e in entries])
+    for algo in (0, 1):
+        sq = [po.scores(algo, qv, db, off, M, -5, -2) for qv in (qf, qr)]
+        chunk = 37
+        order_s, order_i = [], []
+        e0 = 0
+        while e0 < len(entries):
+            cend = (entries[e0][0] // chunk + 1) * chunk
+            e1 = e0
+            while e1 < len(entries) and entries[e1][0] < cend:
+                e1 += 1
+            for v in range(2):
+                for e in range(e0, e1):
+                    order_s.append(sq[v][e])
+                    order_i.append(entries[e][0])
+            e0 = e1
+        exp = po.topk(np.array(order_s), np.array(order_i, np.uint64), 25)
+        configure(True, ("const", 2, -3), -5, -2, chunk=chunk, strands=S.BOTH_STRANDS)
+        with tempfile.TemporaryDirectory() as tmp:
+            path = os.path.join(tmp, "db.fas")
+            with open(path, "wb") as f:
+                for s in seqs:
+                    f.write(b">x\n" + s + b"\n")
+            S.init_db(path)
+            qq = S.init_sequence_fasta(S.READ_FROM_STRING, qraw.decode())
+            fn = S.sw_align if algo == 0 else S.nw_align
+            got = [(h["score"], h["id"]) for h in fn(qq, 25, 16)]
+            S.free_sequence(qq)
+        assert [s for s, _ in got] == [s for s, _ in exp]
+        assert got == exp
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+    S.set_chunk_size(1000)
