@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark: GCUPS of the SW int16 database search on MI355X (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): Smith-Waterman, BLOSUM62, gaps -11/-1,
+one 400-residue query against a synthetic 1 M-sequence protein DB (lengths
+1+Gamma(2,175) clipped to [16,4096], BLOSUM62 background, planted homologs;
+libssa_amd/synthetic.py), top-k = 10.  A step is one search: at N=1 the
+public sw_align() call (DB already packed in HBM, as the reference times
+sw_align with the DB pre-loaded, benchmark/src/benchmark_util.c:27-48); at
+N>1 each rank searches its own 1 M-sequence shard of an N M-sequence DB
+(weak scaling: global IDs rank*1M + i), returns its exact top-k insertion
+log, the logs are gathered to rank 0 over RCCL and replayed there
+(ssa_amd_replay), giving the bit-exact global result.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--seqs S] [--algo sw|nw]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_LANE_OPS = 256 * 128 * 2.4e9   # 256 CUs x 128 lanes/clk x 2.4 GHz (32-bit lane-ops/s)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--seqs", type=int, default=1_000_000, help="DB sequences per GPU")
+    p.add_argument("--qlen", type=int, default=400)
+    p.add_argument("--algo", default="sw", choices=["sw", "nw"])
+    p.add_argument("--matrix", default="blosum62")
+    p.add_argument("--gap-open", type=int, default=-11)
+    p.add_argument("--gap-extend", type=int, default=-1)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--strip-np", type=int, default=16)
+    return p.parse_args()
+
+
+def cpu_baseline(codes, off, q, M, args, cores):
+    """The reference's own AVX2 int16 kernel (search_16_chunk ->
+    search_16_avx2_sw, compiled from its sources into oracle/_ref) timed on
+    the host cores over a bounded sample; falls back to the int64 oracle
+    port when the reference build is absent."""
+    from oracle import pyoracle as po
+    algo = 0 if args.algo == "sw" else 1
+    n = len(off) - 1
+    if po.have_ref():
+        # size the sample to ~cpu_seconds at a conservative 8 GCUPS/thread
+        cells_per_seq = float(off[-1]) / n * len(q)
+        sample = int(min(n, max(1000, args.cpu_seconds * 8e9 * cores / cells_per_seq)))
+        soff = off[:sample + 1]
+        hits, _, ns, secs = po.ref_run(po.MODE_SEARCH16_AVX2, algo, q, None, M, args.gap_open, args.gap_extend,
+                                       k=args.k, threads=cores, repeat=3, db_off=(codes, soff))
+        cells = float(soff[-1]) * len(q)
+        return {"value": cells / secs / 1e9, "unit": "GCUPS", "cores": cores, "kind": "reference",
+                "sample": f"first {sample} of {n} DB sequences ({cells:.3g} cells), reference AVX2 int16 "
+                          f"search_16_chunk on {cores} threads, chunk 1000, k={args.k}"}
+    po.build(quiet=True)
+    sample = 2000
+    soff = off[:sample + 1]
+    t0 = time.perf_counter()
+    po.scores(algo, q, codes[:int(soff[-1])], soff, M, args.gap_open, args.gap_extend, threads=cores)
+    secs = time.perf_counter() - t0
+    cells = float(soff[-1]) * len(q)
+    return {"value": cells / secs / 1e9, "unit": "GCUPS", "cores": cores, "kind": "port",
+            "sample": f"first {sample} DB sequences, oracle int64 scalar port on {cores} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import libssa_amd as S
+    from libssa_amd import synthetic as syn
+
+    S.load()
+    S.set_device(local)
+    S.set_output_mode(S.OUTPUT_ERROR)
+    S.set_option("strip_np", args.strip_np)
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+    S.init_score_matrix(S.MATRIX_BUILDIN, args.matrix)
+    S.init_gap_penalties(args.gap_open, args.gap_extend)
+    algo = S.SW if args.algo == "sw" else S.NW
+
+    # --- synthetic shard (untimed): generate, write FASTA, pack into HBM
+    t0 = time.time()
+    q = syn.protein_query(args.qlen, 7)
+    codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000)
+    tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
+    path = os.path.join(tmpdir, "db.fas")
+    syn.write_fasta(path, codes, off)
+    S.init_db(path)
+    S.set_id_offset(rank * args.seqs)
+    S.prepare_db()
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    setup_s = time.time() - t0
+    cells_local = float(off[-1]) * args.qlen
+
+    def step():
+        if world == 1:
+            fn = S.sw_align if algo == S.SW else S.nw_align
+            return [(h["score"], h["id"]) for h in fn(qq, args.k, S.BIT_WIDTH_16)]
+        import torch
+        log = S.search(qq, algo, args.k, S.BIT_WIDTH_16, S.LOG)
+        t = torch.tensor([[h[0], h[1]] for h in log] or [[0, 0]], dtype=torch.int64, device="cuda")
+        n = torch.tensor([len(log)], dtype=torch.int64, device="cuda")
+        lens = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(lens, n)
+        mx = int(max(x.item() for x in lens)) or 1
+        pad = torch.zeros((mx, 2), dtype=torch.int64, device="cuda")
+        pad[: t.shape[0]] = t[:mx]
+        gl = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, gl, dst=0)
+        if rank == 0:
+            merged = []
+            for r in range(world):
+                merged += [tuple(x) for x in gl[r][: int(lens[r].item())].tolist()]
+            return S.replay(merged, args.k)
+        return None
+
+    def sync():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    kernel_ms, wide_ms = [], []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        st = S.stats()
+        kernel_ms.append(st["kernel_ms"])
+        wide_ms.append(st["wide_ms"])
+    sync()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = S.stats()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    total_cells = cells_local * world
+    ms_per_step = elapsed / args.steps * 1e3
+    gcups = total_cells / (elapsed / args.steps) / 1e9
+    kavg = float(np.mean(kernel_ms))
+    # algorithmic bytes per launch: every residue once (1 B) + 4 B score per
+    # sequence + the strip profile table
+    alg_bytes = float(st["kernel_bytes"])
+    achieved = alg_bytes / (kavg * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}")
+        except Exception:
+            traffic = None
+    ops_per_cell = 5.35 if args.algo == "sw" else 5.6   # VALU lane-instructions per cell (kernel ISA)
+    out = {
+        "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
+        "value": round(gcups, 2),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "i16",
+        "data": "synthetic",
+        "config": {"workload": f"{args.algo.upper()} int16 {args.matrix} gaps {args.gap_open}/{args.gap_extend}, "
+                               f"{args.qlen}-aa query vs {args.seqs} synthetic protein seqs per GPU "
+                               f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
+                   "db_seqs_per_gpu": args.seqs, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
+                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "strip_np": args.strip_np},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+        "kernel": {"name": "strip16_kernel", "avg_ms": round(kavg, 4),
+                   "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
+                   "wide_ms_avg": round(float(np.mean(wide_ms)), 4),
+                   "valu_bound_gcups": round(VALU_LANE_OPS / ops_per_cell / 1e9, 1),
+                   "valu_frac": (cells_local / (kavg * 1e-3)) / (VALU_LANE_OPS / ops_per_cell)},
+        "setup_s": round(setup_s, 1),
+        "top_hit": list(res[0]) if res else None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import pyoracle as po
+        tabs = np.load(os.path.join(ROOT, "tests", "golden", "tables.npz"))
+        M = tabs["matrices"][[str(x) for x in tabs["names"]].index(args.matrix)].copy()
+        cores = min(16, os.cpu_count() or 1)
+        try:
+            out["cpu_baseline"] = cpu_baseline(codes, off, q, M, args, cores)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
