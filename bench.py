@@ -28,7 +28,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_LANE_OPS = 256 * 128 * 2.4e9   # 256 CUs x 128 lanes/clk x 2.4 GHz (32-bit lane-ops/s)
 
 
 def parse():
@@ -84,12 +83,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks on one GPU
     dist = None
+    backend = os.environ.get("SSA_DIST_BACKEND", "nccl")   # nccl == RCCL on ROCm; gloo for rehearsal
+    dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
 
     import libssa_amd as S
     from libssa_amd import synthetic as syn
@@ -121,23 +125,9 @@ def main():
         if world == 1:
             fn = S.sw_align if algo == S.SW else S.nw_align
             return [(h["score"], h["id"]) for h in fn(qq, args.k, S.BIT_WIDTH_16)]
-        import torch
+        from libssa_amd.dist import global_topk
         log = S.search(qq, algo, args.k, S.BIT_WIDTH_16, S.LOG)
-        t = torch.tensor([[h[0], h[1]] for h in log] or [[0, 0]], dtype=torch.int64, device="cuda")
-        n = torch.tensor([len(log)], dtype=torch.int64, device="cuda")
-        lens = [torch.zeros_like(n) for _ in range(world)]
-        dist.all_gather(lens, n)
-        mx = int(max(x.item() for x in lens)) or 1
-        pad = torch.zeros((mx, 2), dtype=torch.int64, device="cuda")
-        pad[: t.shape[0]] = t[:mx]
-        gl = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
-        dist.gather(pad, gl, dst=0)
-        if rank == 0:
-            merged = []
-            for r in range(world):
-                merged += [tuple(x) for x in gl[r][: int(lens[r].item())].tolist()]
-            return S.replay(merged, args.k)
-        return None
+        return global_topk(log, args.k, dist, rank, world, dev)
 
     def sync():
         if dist is not None:
@@ -159,7 +149,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st = S.stats()
@@ -177,11 +167,16 @@ def main():
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}")
-        except Exception:
-            traffic = None
-    ops_per_cell = 5.35 if args.algo == "sw" else 5.6   # VALU lane-instructions per cell (kernel ISA)
+        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_np{args.strip_np}")
+        if rec:
+            traffic = rec["bytes_per_launch"]
+    # VALU issue roofline: the strip kernel is made of
+    # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
+    # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
+    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_c2_sw_np16).
+    instr_per_cell = {("sw", 16): 5.59}.get((args.algo, args.strip_np))
+    issue_cycles = 4.17
+    valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
         "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
         "value": round(gcups, 2),
@@ -205,8 +200,9 @@ def main():
         "kernel": {"name": "strip16_kernel", "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
                    "wide_ms_avg": round(float(np.mean(wide_ms)), 4),
-                   "valu_bound_gcups": round(VALU_LANE_OPS / ops_per_cell / 1e9, 1),
-                   "valu_frac": (cells_local / (kavg * 1e-3)) / (VALU_LANE_OPS / ops_per_cell)},
+                   "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,
+                   "valu_issue_frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None,
+                   "valu_instr_per_cell": instr_per_cell},
         "setup_s": round(setup_s, 1),
         "top_hit": list(res[0]) if res else None,
     }

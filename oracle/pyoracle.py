@@ -49,6 +49,8 @@ def lib():
                                     ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.oracle_topk.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, P, P]
         L.oracle_topk.restype = ctypes.c_size_t
+        L.oracle_topk_log.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, P, P]
+        L.oracle_topk_log.restype = ctypes.c_size_t
         L.oracle_map_db.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, P]
         L.oracle_map_db.restype = ctypes.c_size_t
         L.oracle_map_query.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, P]
@@ -156,6 +158,16 @@ def topk(sc: np.ndarray, ids: np.ndarray, k: int) -> list[tuple[int, int]]:
     os_ = np.zeros(max(k, 1), dtype=np.int64)
     oi = np.zeros(max(k, 1), dtype=np.uint64)
     c = lib().oracle_topk(_ptr(sc), _ptr(ids), len(sc), k, _ptr(os_), _ptr(oi))
+    return [(int(os_[i]), int(oi[i])) for i in range(c)]
+
+
+def topk_log(sc: np.ndarray, ids: np.ndarray, k: int) -> list[tuple[int, int]]:
+    """Elements the reference heap accepts, in insertion order."""
+    sc = np.ascontiguousarray(sc, dtype=np.int64)
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    os_ = np.zeros(max(len(sc), 1), dtype=np.int64)
+    oi = np.zeros(max(len(sc), 1), dtype=np.uint64)
+    c = lib().oracle_topk_log(_ptr(sc), _ptr(ids), len(sc), k, _ptr(os_), _ptr(oi))
     return [(int(os_[i]), int(oi[i])) for i in range(c)]
 
 

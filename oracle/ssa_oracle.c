@@ -258,8 +258,8 @@ void oracle_scores(int algo, const uint8_t* db, const uint64_t* offsets, size_t 
  * (CMP_ASC in util.h:12 sorts descending; minheap.c:93-106). */
 typedef struct { int64_t score; uint64_t id; } ent_t;
 
-static void heap_add(ent_t* a, size_t* count, size_t alloc, ent_t n) {
-    if (alloc == 0) return;
+static int heap_add(ent_t* a, size_t* count, size_t alloc, ent_t n) {
+    if (alloc == 0) return 0;
     if (*count < alloc) {
         size_t i = (*count)++;
         while (i > 0) {
@@ -269,6 +269,7 @@ static void heap_add(ent_t* a, size_t* count, size_t alloc, ent_t n) {
             i = p;
         }
         a[i] = n;
+        return 1;
     } else if (a[0].score < n.score) {
         size_t p = 0, c = 1;
         while (c < *count) {
@@ -279,7 +280,9 @@ static void heap_add(ent_t* a, size_t* count, size_t alloc, ent_t n) {
             c = 2 * p + 1;
         }
         a[p] = n;
+        return 1;
     }
+    return 0;
 }
 
 static int ent_cmp(const void* x, const void* y) {
@@ -304,4 +307,19 @@ size_t oracle_topk(const int64_t* scores, const uint64_t* ids, size_t n, size_t 
     for (size_t i = 0; i < count; i++) { out_scores[i] = a[i].score; out_ids[i] = a[i].id; }
     free(a);
     return count;
+}
+
+/* Insertion log: the elements the heap accepts, in insertion order (used to
+ * check the sharded exchange: any globally accepted element is accepted by
+ * its shard's heap). Returns the log length. */
+size_t oracle_topk_log(const int64_t* scores, const uint64_t* ids, size_t n, size_t k,
+                       int64_t* log_scores, uint64_t* log_ids) {
+    ent_t* a = (ent_t*)malloc(sizeof(ent_t) * (k ? k : 1));
+    size_t count = 0, m = 0;
+    for (size_t i = 0; i < n; i++) {
+        ent_t e = {scores[i], ids[i]};
+        if (heap_add(a, &count, k, e)) { log_scores[m] = e.score; log_ids[m] = e.id; m++; }
+    }
+    free(a);
+    return m;
 }

@@ -1,0 +1,73 @@
+"""Multi-process exchange of a sharded search on CPU (gloo, world size 2 and 3).
+
+Each rank scores its contiguous ID shard with the oracle, builds the shard's
+insertion log (what ssa_amd_search(..., SSA_AMD_LOG) returns on a GPU), and
+the ranks run the production exchange (libssa_amd.dist: all_gather of log
+lengths + one gather + ssa_amd_replay on rank 0).  Rank 0's result must equal
+the single-process 64-bit reference top-k, tie IDs included.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from libssa_amd import synthetic as syn
+from oracle import pyoracle as po
+from tests.conftest import GOLDEN
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cuts, k, outdir):
+    import torch.distributed as dist
+    import libssa_amd as S
+    from libssa_amd.dist import global_topk
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    S.load()
+    q = syn.protein_query(50, 1)
+    codes, off = syn.protein_db(3000, 4, query=q, plant_every=200, lo=0, hi=150)
+    tabs = np.load(os.path.join(GOLDEN, "tables.npz"))
+    M = tabs["matrices"][2].copy()  # blosum62
+    a, b = cuts[rank], cuts[rank + 1]
+    sc = po.scores(0, q, codes, off, M, -11, -1)[a:b]
+    lens = np.diff(off)[a:b]
+    keep = np.nonzero(lens > 0)[0]
+    log = po.topk_log(sc[keep], (keep + a).astype(np.uint64), k)
+    res = global_topk([(s, i, 0, 0, 0) for s, i in log], k, dist, rank, world, "cpu")
+    if rank == 0:
+        allsc = po.scores(0, q, codes, off, M, -11, -1)
+        nz = np.nonzero(np.diff(off) > 0)[0]
+        exp = po.topk(allsc[nz], nz.astype(np.uint64), k)
+        with open(os.path.join(outdir, f"r{k}.txt"), "w") as f:
+            f.write("ok" if res == exp else f"mismatch {res[:5]} {exp[:5]}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cuts", [(2, [0, 1500, 3000]), (3, [0, 7, 2222, 3000])])
+@pytest.mark.parametrize("k", [1, 10, 137])
+def test_gloo_gather_replay_equals_single_process(tmp_path, world, cuts, k):
+    mp.spawn(_worker, args=(world, _free_port(), cuts, k, str(tmp_path)), nprocs=world, join=True)
+    assert open(tmp_path / f"r{k}.txt").read() == "ok"
+
+
+def test_shard_log_property():
+    """Every element accepted by the global heap is in its shard's log."""
+    rng = np.random.default_rng(1)
+    sc = rng.integers(0, 30, 4000)
+    ids = np.arange(4000, dtype=np.uint64)
+    for k in (1, 5, 64):
+        glob = set(po.topk_log(sc, ids, k))
+        shards = set()
+        for a, b in ((0, 1000), (1000, 3333), (3333, 4000)):
+            shards |= set(po.topk_log(sc[a:b], ids[a:b], k))
+        assert glob <= shards

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Turns a tools/profile_pmc.sh output directory into the per-launch HBM
+traffic figure bench.py reports as roofline.traffic (profiles/traffic.json).
+
+Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly half
+the bytes of a wide coalesced streaming read on gfx950 -> x2; WRITE_SIZE is
+exact for 16-B-per-lane streaming stores.  Both kernels' loads and stores are
+16 B per lane, fully coalesced."""
+import csv
+import json
+import os
+import sys
+
+
+def mean_counter(d, name):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
+            if r["Counter_Name"] == name]
+    return sum(vals) / len(vals)
+
+
+def main():
+    pmc_dir, key = sys.argv[1], sys.argv[2]
+    fetch = mean_counter(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE") * 1024 * 2
+    write = mean_counter(os.path.join(pmc_dir, "write"), "WRITE_SIZE") * 1024
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "profiles", "traffic.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    data[key] = {"bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
+                 "source": os.path.relpath(pmc_dir, root)}
+    json.dump(data, open(path, "w"), indent=1)
+    print(key, data[key])
+
+
+if __name__ == "__main__":
+    main()
