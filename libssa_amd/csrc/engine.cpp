@@ -320,11 +320,14 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         const bool fits16 = minM >= -32768 && maxM <= 32767;
         uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(m, Q, R, minM, maxM) : 0xffffffffu) : 0;
         if (C.force_wide) nmax16 = 0;
+        // SW on f16 bit patterns (strip_f16m_kernel) needs non-positive gaps and
+        // scores within +-1024 so no pattern can leave [0x0400, 0x7C7F]
+        const bool use_f16 = !nw && C.sw_kernel == 0 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024;
 
         // strip profile table: dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
         std::vector<uint32_t> qpt((size_t)nstrips * 32 * np);
-        const int16_t padv = nw ? 0 : -32768;
+        const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
         auto val = [&](int c, size_t i) -> int16_t {
             if (c == kPadCode || i >= m) return padv;
             const int64_t x = M[(c << 5) + qv.seq[i]];
@@ -376,6 +379,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         a.gap_extend = R;
         a.nmax16 = nmax16;
         a.ovf_cap = (uint32_t)kOvfCap;
+        a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
 
         WideArgs w{};
         w.res = D.d_res;
@@ -394,7 +398,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         w.ovf_cap = (uint32_t)kOvfCap;
 
         check(hipEventRecord(D.ev[0], st), "event");
-        check(launch_strip16(a, np, nw, st), "strip16 kernel launch");
+        check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         check(hipEventRecord(D.ev[1], st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         check(hipEventRecord(D.ev[2], st), "event");

@@ -7,6 +7,7 @@ namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
 constexpr uint8_t kPadCode = 31;   // residue code of padding columns (never a real residue)
+constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
 struct GroupDesc {
     uint32_t blk;     // residue offset in 1 KiB blocks (16 columns x 64 lanes)
@@ -27,6 +28,7 @@ struct StripArgs {
     int32_t gap_open, gap_extend;
     uint32_t nmax16;           // longest DB entry proven int16-safe
     uint32_t ovf_cap;          // capacity of ovf_list
+    uint32_t pad_word;         // profile dword of the padding residue (both halves)
 };
 
 struct WideArgs {
@@ -46,6 +48,7 @@ struct WideArgs {
 };
 
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
+hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
 }  // namespace ssa

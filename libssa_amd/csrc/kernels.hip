@@ -259,6 +259,165 @@ strip16_kernel(const StripArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// SW on order-preserving f16 bit patterns.
+//
+// Same strip / skew / LDS-profile structure as strip16_kernel, but every value
+// is kept as the 16-bit pattern v + kF16Floor (v = true SW value >= 0), which
+// orders like the f16 number it encodes as long as it stays in
+// [0x0400, 0x7BFF] (positive normals).  That buys:
+//   * v_pk_maximum3_f16: one half-rate instruction takes the max of THREE
+//     packed operands (H = max(diag, E, F); S over two rows at once);
+//   * the constant gap adds (T = H+Q+R, E+R, F+R) never carry between the
+//     halves, so they run as full-rate v_add_u32 on the packed pair;
+//   * the local-alignment floor is the constant kF16Floor in E's max3.
+// Nothing can wrap: every increment is bounded by the floor (host checks
+// |score| <= 1024, Q,R <= 0), so no pattern drops below 0x0400 (no
+// denormals, no zeros).  Only an overflowing score pushes a pattern to
+// 0x7C00+ (inf/NaN), which v_pk_maximum3_f16 propagates into S; such lanes
+// go to wide_kernel.  Exact scores up to 0x7BFF - kF16Floor = 29695.
+// ---------------------------------------------------------------------------
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t fmax3(uint32_t a, uint32_t b, uint32_t c) {
+    const h2 m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_bit_cast(h2, a),
+                                                                            __builtin_bit_cast(h2, b)),
+                                               __builtin_bit_cast(h2, c));
+    return __builtin_bit_cast(uint32_t, m);
+}
+__device__ __forceinline__ uint32_t fmax2(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(h2, a),
+                                                                      __builtin_bit_cast(h2, b)));
+}
+__device__ __forceinline__ uint32_t padd16(uint32_t a, uint32_t b) {   // v_pk_add_u16 (wrapping)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, a) + __builtin_bit_cast(u2, b));
+}
+
+template <int NP>
+__global__ void __launch_bounds__(64 * kWaves)
+strip_f16m_kernel(const StripArgs a) {
+    constexpr int ROWW = NP + 4;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[kWaves][32 * ROWW];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t g = blockIdx.x * kWaves + wave;
+    if (g >= a.ngroups) return;
+
+    uint32_t* lds = lds_all[wave];
+    const GroupDesc gd = a.groups[g];
+    const uint32_t nblk = gd.ncols >> 4;
+    const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
+    uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
+    const uint32_t gl = g * 64 + lane;
+    const uint32_t len = a.lane_len[gl];
+
+    constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;   // floor pattern in both halves
+    const int QR = a.gap_open + a.gap_extend, R = a.gap_extend;
+    // packed constants in "combined" form so one 32-bit add updates both halves
+    const uint32_t cQR = (uint32_t)(QR * 65536 + QR);
+    const uint32_t cR = (uint32_t)(R * 65536 + R);
+
+    uint32_t S = FL;
+
+    for (int s = 0; s < (int)a.nstrips; s++) {
+        const uint32_t* src = a.qpt + (size_t)s * 32 * NP;
+#pragma unroll
+        for (int i = 0; i < (32 * NP) / 64; i++) {
+            const int idx = i * 64 + lane;
+            lds[(idx / NP) * ROWW + (idx % NP)] = src[idx];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const bool first = (s == 0);
+
+        uint32_t H[NP], E[NP], prevw[NP];
+#pragma unroll
+        for (int r = 0; r < NP; r++) {
+            H[r] = FL;
+            E[r] = FL;
+            prevw[r] = a.pad_word;      // profile of the virtual residue before column 0
+        }
+        uint32_t hd0 = FL, Fprev = FL;
+        uint32_t ob[4] = {0, 0, 0, 0};
+        uint4 rnext = resp[0];
+        uint4 qnext = first ? make_uint4(0, 0, 0, 0) : rbp[0];
+        uint32_t nxt[NP];
+        load_row<NP>(nxt, lds + (rnext.x & 0xffu) * ROWW);
+
+        for (uint32_t b = 0; b < nblk; b++) {
+            const uint4 rcur = rnext;
+            if (b + 1 < nblk) rnext = resp[(size_t)(b + 1) * 64];
+            const uint32_t rw[4] = {rcur.x, rcur.y, rcur.z, rcur.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint4 qcur = qnext;
+                if (!first) {
+                    const uint32_t nq = b * 4 + t + 1;
+                    if (nq < nblk * 4) qnext = rbp[(size_t)nq * 64];
+                }
+                const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = t * 4 + u;
+                    uint32_t cur[NP];
+#pragma unroll
+                    for (int r = 0; r < NP; r++) cur[r] = nxt[r];
+                    {
+                        const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
+                                                   : (rnext.x & 0xffu);
+                        load_row<NP>(nxt, lds + dn * ROWW);
+                    }
+                    const uint32_t rbv = first ? FL : qw[u];
+                    uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
+                    uint32_t hd = hd0;
+#pragma unroll
+                    for (int r = 0; r < NP; r++) {
+                        const uint32_t P = (cur[r] & 0xffffu) | (prevw[r] & 0xffff0000u);
+                        const uint32_t h = fmax3(padd16(hd, P), E[r], F);
+                        hd = H[r];
+                        H[r] = h;
+                        const uint32_t tt = h + cQR;
+                        E[r] = fmax3(E[r] + cR, tt, FL);
+                        F = fmax2(F + cR, tt);
+                        prevw[r] = cur[r];
+                        if (r & 1) S = fmax3(S, H[r - 1], H[r]);
+                    }
+                    hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
+                    Fprev = F;
+                    asm volatile("" : "+v"(S));
+                    if (!(b == 0 && k == 0)) {
+                        ob[(k + 3) & 3] = perm(F, H[NP - 1], SEL_LO_BHI_HI_AHI);
+                        if ((k & 3) == 0)
+                            rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        ob[3] = FL;
+        rbp[(size_t)(nblk * 4 - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    const uint32_t o = a.lane_out[gl];
+    if (o == 0xffffffffu) return;
+    if (len == 0) {
+        a.scores[o] = 0;
+        return;
+    }
+    const uint32_t slo = S & 0xffffu, shi = S >> 16;
+    const uint32_t smax = slo > shi ? slo : shi;          // patterns order as integers
+    const bool ovf = smax >= 0x7C00u || len > a.nmax16;
+    if (ovf) {
+        const uint32_t idx = atomicAdd(a.ovf_count, 1u);
+        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;
+        a.scores[o] = INT32_MIN;
+    } else {
+        a.scores[o] = (int32_t)smax - kF16Floor;
+    }
+}
+
 // Exact int64 re-score of overflowed lanes: the reference's 64-bit
 // recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
@@ -344,6 +503,15 @@ hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st) {
     if (np == 8) return nw ? launch_np<8, true>(a, st) : launch_np<8, false>(a, st);
     if (np == 32) return nw ? launch_np<32, true>(a, st) : launch_np<32, false>(a, st);
     return nw ? launch_np<16, true>(a, st) : launch_np<16, false>(a, st);
+}
+
+hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
+    const uint32_t blocks = (a.ngroups + kWaves - 1) / kWaves;
+    if (blocks == 0) return hipSuccess;
+    if (np == 8) hipLaunchKernelGGL((strip_f16m_kernel<8>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    else if (np == 32) hipLaunchKernelGGL((strip_f16m_kernel<32>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    else hipLaunchKernelGGL((strip_f16m_kernel<16>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

@@ -132,12 +132,63 @@ def test_query_length_edges_vs_oracle(qlen, algo):
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
-        for np_ in (8, 16, 32):
-            S.set_option("strip_np", np_)
-            sc, ids = _full_scores(qq, algo, len(keep))
-            assert (ids == keep).all()
-            assert (sc == exp).all(), (np_, np.nonzero(sc != exp)[0][:10])
+        for swk in ((0, 1) if algo == S.SW else (0,)):
+            S.set_option("sw_kernel", swk)
+            for np_ in (8, 16, 32):
+                S.set_option("strip_np", np_)
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all()
+                assert (sc == exp).all(), (swk, np_, np.nonzero(sc != exp)[0][:10])
         S.set_option("strip_np", 16)
+        S.set_option("sw_kernel", 0)
+        S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("match", [40, 55, 127])
+def test_sw_f16_pattern_limit(match):
+    """Scores around the f16-pattern kernel's exact range (29695) and the
+    int16 range (65534): every score still exact (re-routed lanes)."""
+    rng = np.random.default_rng(match)
+    base = rng.choice(syn.AA_CODES, size=1200).astype(np.uint8)
+    seqs = [base[:n] for n in (200, 500, 540, 560, 600, 700, 1200)] + [rng.choice(syn.AA_CODES, 300).astype(np.uint8)]
+    codes = np.concatenate(seqs)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    M = po.matrix_constant(match, -1)
+    exp = po.scores(0, base, codes, off, M, -3, -1)
+    configure(False, ("const", match, -1), -3, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(base))
+        for swk in (0, 1):
+            S.set_option("sw_kernel", swk)
+            sc, _ = _full_scores(qq, S.SW, len(seqs))
+            assert (sc == exp).all(), (swk, sc, exp)
+        S.set_option("sw_kernel", 0)
+        S.free_sequence(qq)
+
+
+def test_sw_large_matrix_values_fall_back(tmp_path):
+    """|score| > 1024 is outside the f16-pattern kernel's contract: the
+    engine must pick the int16 kernel (or int64) and stay exact."""
+    txt = "   A  R  N\nA 2000 -5 -1500\nR -5 7 -1\nN -1500 -1 6\n"
+    mpath = tmp_path / "big.txt"
+    mpath.write_text(txt)
+    M = po.matrix_parse(txt)
+    rng = np.random.default_rng(7)
+    alpha = np.array([1, 16, 13], np.uint8)   # A R N codes
+    q = rng.choice(alpha, 90).astype(np.uint8)
+    seqs = [rng.choice(alpha, n).astype(np.uint8) for n in rng.integers(1, 120, 200)]
+    codes = np.concatenate(seqs)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    for algo in (S.SW, S.NW):
+        exp = po.scores(algo, q, codes, off, M, -4, -2)
+        configure(False, ("file", str(mpath)), -4, -2)
+        S.init_db(_write_db(str(tmp_path), codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        sc, _ = _full_scores(qq, algo, len(seqs))
+        assert (sc == exp).all()
         S.free_sequence(qq)
 
 
