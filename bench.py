@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--strip-np", type=int, default=16)
+    p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
     return p.parse_args()
 
 
@@ -102,6 +103,9 @@ def main():
     S.set_device(local)
     S.set_output_mode(S.OUTPUT_ERROR)
     S.set_option("strip_np", args.strip_np)
+    for o in args.option:
+        k, v = o.split("=")
+        S.set_option(k, int(v))
     S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
     S.init_score_matrix(S.MATRIX_BUILDIN, args.matrix)
     S.init_gap_penalties(args.gap_open, args.gap_extend)

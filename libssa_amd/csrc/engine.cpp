@@ -195,8 +195,23 @@ void ensure_device_db() {
         blocks += ncols / 16;
     }
     if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
+    // compact alphabet: the residue codes that occur, in code order; the
+    // padding column gets the next code.  Pair-symbol profiles scale with
+    // (alpha+1)^2, so a 20-letter DB uses 441 rows instead of 1024.
+    bool present[256] = {false};
+    for (uint8_t c : S.codes) present[c] = true;
+    std::vector<uint8_t> code_of;
+    uint8_t remap[256] = {0};
+    for (int c = 0; c < 256; c++)
+        if (present[c]) {
+            remap[c] = (uint8_t)code_of.size();
+            code_of.push_back((uint8_t)c);
+        }
+    if (code_of.size() > 31) fatal("residue alphabet too large (%d codes)", (int)code_of.size());
+    const uint8_t pad = (uint8_t)code_of.size();
+    for (auto& c : S.codes) c = remap[c];
     std::vector<uint32_t> lane_len((size_t)ngroups * 64, 0), lane_out((size_t)ngroups * 64, 0xffffffffu);
-    std::vector<uint8_t> res((size_t)blocks * 1024, kPadCode);
+    std::vector<uint8_t> res((size_t)blocks * 1024, pad);
     const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;
     for (unsigned t = 0; t < nth; t++) {
@@ -242,6 +257,8 @@ void ensure_device_db() {
     D.nblocks = blocks;
     D.meta = std::move(S.meta);
     D.lane_out = std::move(lane_out);
+    D.code_of = std::move(code_of);
+    D.alpha = pad;
     D.generation = C.db_generation;
     D.symtype = C.symtype;
     D.strands = C.strands;
@@ -309,37 +326,61 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
                 hs[e] = nw ? (int32_t)(Q + (int64_t)D.meta.len[e] * R) : 0;
             continue;
         }
-        // profile bounds over every residue code a DB entry can hold
+        // profile bounds over the residue codes the DB holds
+        const uint32_t A = D.alpha;
         int64_t minM = INT64_MAX, maxM = INT64_MIN;
         for (size_t i = 0; i < m; i++)
-            for (int c = 0; c < 31; c++) {
-                const int64_t x = M[(c << 5) + qv.seq[i]];
+            for (uint32_t c = 0; c < A; c++) {
+                const int64_t x = M[(D.code_of[c] << 5) + qv.seq[i]];
                 minM = std::min(minM, x);
                 maxM = std::max(maxM, x);
             }
+        if (A == 0) minM = maxM = 0;
         const bool fits16 = minM >= -32768 && maxM <= 32767;
         uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(m, Q, R, minM, maxM) : 0xffffffffu) : 0;
         if (C.force_wide) nmax16 = 0;
-        // SW on f16 bit patterns (strip_f16m_kernel) needs non-positive gaps and
-        // scores within +-1024 so no pattern can leave [0x0400, 0x7C7F]
-        const bool use_f16 = !nw && C.sw_kernel == 0 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024;
+        // SW on f16 bit patterns needs non-positive gaps and scores within
+        // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
+        const bool use_f16 = !nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024;
+        // pair-symbol profile (sw_pair_kernel): (alpha+1)^2 rows in LDS
+        const uint32_t prow = A + 1;
+        const size_t pair_lds = (size_t)prow * prow * (np + 4) * 4;
+        const bool use_pair = use_f16 && C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax;
 
-        // strip profile table: dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r])
+        // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
+        // pair table, dword (s, c1*prow+c0, r) = (QP[c1][s*2np+r], QP[c0][s*2np+np+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
-        std::vector<uint32_t> qpt((size_t)nstrips * 32 * np);
         const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
-        auto val = [&](int c, size_t i) -> int16_t {
-            if (c == kPadCode || i >= m) return padv;
-            const int64_t x = M[(c << 5) + qv.seq[i]];
+        auto val = [&](uint32_t c, size_t i) -> int16_t {
+            if (c >= A || i >= m) return padv;
+            const int64_t x = M[(D.code_of[c] << 5) + qv.seq[i]];
             return (int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, x));
         };
-        for (uint32_t s = 0; s < nstrips; s++)
-            for (int c = 0; c < 32; c++)
-                for (int r = 0; r < np; r++) {
-                    const size_t i = (size_t)s * 2 * np + r;
-                    qpt[((size_t)s * 32 + c) * np + r] =
-                        (uint32_t)(uint16_t)val(c, i) | ((uint32_t)(uint16_t)val(c, i + np) << 16);
-                }
+        std::vector<uint32_t> qpt;
+        if (use_pair) {
+            qpt.resize((size_t)nstrips * prow * prow * np);
+            for (uint32_t s = 0; s < nstrips; s++)
+                for (uint32_t c1 = 0; c1 < prow; c1++)
+                    for (uint32_t c0 = 0; c0 < prow; c0++)
+                        for (int r = 0; r < np; r++) {
+                            const size_t i = (size_t)s * 2 * np + r;
+                            qpt[(((size_t)s * prow + c1) * prow + c0) * np + r] =
+                                (uint32_t)(uint16_t)val(c1, i) | ((uint32_t)(uint16_t)val(c0, i + np) << 16);
+                        }
+        } else {
+            qpt.resize((size_t)nstrips * 32 * np);
+            for (uint32_t s = 0; s < nstrips; s++)
+                for (uint32_t c = 0; c < 32; c++)
+                    for (int r = 0; r < np; r++) {
+                        const size_t i = (size_t)s * 2 * np + r;
+                        qpt[((size_t)s * 32 + c) * np + r] =
+                            (uint32_t)(uint16_t)val(c, i) | ((uint32_t)(uint16_t)val(c, i + np) << 16);
+                    }
+        }
+        // the int64 kernel scores compact codes too
+        int64_t Mc[1024];
+        for (int x = 0; x < 32; x++)
+            for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(D.code_of[x] << 5) + y] : -1;
         if (D.qpt_cap < qpt.size()) {
             dfree(D.d_qpt);
             check(hipMalloc((void**)&D.d_qpt, qpt.size() * 4), "qpt");
@@ -359,7 +400,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         hipStream_t st = D.stream;
         check(hipMemcpyAsync(D.d_qpt, qpt.data(), qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
         check(hipMemcpyAsync(D.d_query, qv.seq, m, hipMemcpyHostToDevice, st), "H2D query");
-        check(hipMemcpyAsync(D.d_matrix, M, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        check(hipMemcpyAsync(D.d_matrix, Mc, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
         check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
 
         StripArgs a{};
@@ -380,6 +421,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         a.nmax16 = nmax16;
         a.ovf_cap = (uint32_t)kOvfCap;
         a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
+        a.alpha = A;
 
         WideArgs w{};
         w.res = D.d_res;
@@ -398,7 +440,9 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         w.ovf_cap = (uint32_t)kOvfCap;
 
         check(hipEventRecord(D.ev[0], st), "event");
-        check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
+        check(use_pair ? launch_sw_pair(a, pair_lds, C.pair_waves, st)
+                       : use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st),
+              "strip kernel launch");
         check(hipEventRecord(D.ev[1], st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         check(hipEventRecord(D.ev[2], st), "event");

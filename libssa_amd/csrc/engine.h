@@ -52,6 +52,10 @@ struct DeviceDB {
     int64_t* d_work = nullptr;
     size_t work_cap = 0;
     std::vector<uint32_t> lane_out;       // host copy for overflow mapping
+    // residues are stored in a compact alphabet: device code c < alpha stands
+    // for residue code code_of[c]; code alpha is the padding column
+    std::vector<uint8_t> code_of;
+    uint32_t alpha = 0;
     void release();
 };
 DeviceDB& device_db();

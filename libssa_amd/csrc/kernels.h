@@ -6,7 +6,7 @@
 namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
-constexpr uint8_t kPadCode = 31;   // residue code of padding columns (never a real residue)
+constexpr size_t kPairLdsMax = 80 * 1024;   // pair table budget: two workgroups per CU
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
 struct GroupDesc {
@@ -29,6 +29,7 @@ struct StripArgs {
     uint32_t nmax16;           // longest DB entry proven int16-safe
     uint32_t ovf_cap;          // capacity of ovf_list
     uint32_t pad_word;         // profile dword of the padding residue (both halves)
+    uint32_t alpha;            // compact alphabet size; code alpha = padding column
 };
 
 struct WideArgs {
@@ -49,6 +50,7 @@ struct WideArgs {
 
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
+hipError_t launch_sw_pair(const StripArgs& a, size_t lds_bytes, int waves, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
 }  // namespace ssa

@@ -418,6 +418,150 @@ strip_f16m_kernel(const StripArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// SW, f16 bit patterns (as strip_f16m_kernel) with a PAIR-SYMBOL profile.
+//
+// The packed profile operand of one column is (QP[d_j][r], QP[d_{j-1}][r+NP]):
+// low half for the current residue, high half for the previous one (the skew).
+// Indexing the LDS table by the residue pair (d_j, d_{j-1}) returns that
+// operand directly -- no v_bfi_b32 per cell and no VGPR copy of the previous
+// row.  The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB
+// alphabet, +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is
+// shared by the workgroup's W waves, so the waves step through the
+// strips together (one barrier per strip; groups of a workgroup are adjacent
+// in the length order, so their strip lengths nearly match).
+// ---------------------------------------------------------------------------
+template <int NP, int W>
+__global__ void __launch_bounds__(64 * W, 4)
+sw_pair_kernel(const StripArgs a) {
+    constexpr int ROWW = NP + 4;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t g = blockIdx.x * W + wave;
+    const bool active = g < a.ngroups;
+    const uint32_t gg = active ? g : 0;
+
+    const GroupDesc gd = a.groups[gg];
+    const uint32_t nblk = gd.ncols >> 4;
+    const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
+    uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
+    const uint32_t gl = gg * 64 + lane;
+    const uint32_t prow = a.alpha + 1;
+    const uint32_t ntab4 = prow * prow * (NP / 4);  // 16-B chunks per strip table
+
+    constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;
+    const int QR = a.gap_open + a.gap_extend, R = a.gap_extend;
+    const uint32_t cQR = (uint32_t)(QR * 65536 + QR);
+    const uint32_t cR = (uint32_t)(R * 65536 + R);
+
+    uint32_t S = FL;
+
+    for (int s = 0; s < (int)a.nstrips; s++) {
+        // ---- the whole workgroup stages this strip's pair table
+        __syncthreads();
+        const uint4* src = (const uint4*)(a.qpt + (size_t)s * prow * prow * NP);
+        for (uint32_t i = threadIdx.x; i < ntab4; i += 64 * W) {
+            const uint32_t row = i / (NP / 4), k = i % (NP / 4);
+            *(uint4*)(lds + row * ROWW + 4 * k) = src[i];
+        }
+        __syncthreads();
+        if (!active) continue;
+        const bool first = (s == 0);
+
+        uint32_t H[NP], E[NP];
+#pragma unroll
+        for (int r = 0; r < NP; r++) {
+            H[r] = FL;
+            E[r] = FL;
+        }
+        uint32_t hd0 = FL, Fprev = FL;
+        uint32_t ob[4] = {0, 0, 0, 0};
+        uint4 rnext = resp[0];
+        uint4 qnext = first ? make_uint4(0, 0, 0, 0) : rbp[0];
+        // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
+        uint32_t dprev = a.alpha;
+        uint32_t nxt[NP];
+        {
+            const uint32_t d0 = rnext.x & 0xffu;
+            load_row<NP>(nxt, lds + (d0 * prow + dprev) * ROWW);
+            dprev = d0;
+        }
+
+        for (uint32_t b = 0; b < nblk; b++) {
+            const uint4 rcur = rnext;
+            if (b + 1 < nblk) rnext = resp[(size_t)(b + 1) * 64];
+            const uint32_t rw[4] = {rcur.x, rcur.y, rcur.z, rcur.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint4 qcur = qnext;
+                if (!first) {
+                    const uint32_t nq = b * 4 + t + 1;
+                    if (nq < nblk * 4) qnext = rbp[(size_t)nq * 64];
+                }
+                const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = t * 4 + u;
+                    uint32_t P[NP];
+#pragma unroll
+                    for (int r = 0; r < NP; r++) P[r] = nxt[r];
+                    {
+                        const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
+                                                   : (rnext.x & 0xffu);
+                        load_row<NP>(nxt, lds + (dn * prow + dprev) * ROWW);
+                        dprev = dn;
+                    }
+                    const uint32_t rbv = first ? FL : qw[u];
+                    uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
+                    uint32_t hd = hd0;
+#pragma unroll
+                    for (int r = 0; r < NP; r++) {
+                        const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
+                        hd = H[r];
+                        H[r] = h;
+                        const uint32_t tt = h + cQR;
+                        E[r] = fmax3(E[r] + cR, tt, FL);
+                        F = fmax2(F + cR, tt);
+                        if (r & 1) S = fmax3(S, H[r - 1], H[r]);
+                    }
+                    hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
+                    Fprev = F;
+                    asm volatile("" : "+v"(S));
+                    if (!(b == 0 && k == 0)) {
+                        ob[(k + 3) & 3] = perm(F, H[NP - 1], SEL_LO_BHI_HI_AHI);
+                        if ((k & 3) == 0)
+                            rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        ob[3] = FL;
+        rbp[(size_t)(nblk * 4 - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+    }
+
+    if (!active) return;
+    const uint32_t len = a.lane_len[gl];
+    const uint32_t o = a.lane_out[gl];
+    if (o == 0xffffffffu) return;
+    if (len == 0) {
+        a.scores[o] = 0;
+        return;
+    }
+    const uint32_t slo = S & 0xffffu, shi = S >> 16;
+    const uint32_t smax = slo > shi ? slo : shi;
+    const bool ovf = smax >= 0x7C00u || len > a.nmax16;
+    if (ovf) {
+        const uint32_t idx = atomicAdd(a.ovf_count, 1u);
+        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;
+        a.scores[o] = INT32_MIN;
+    } else {
+        a.scores[o] = (int32_t)smax - kF16Floor;
+    }
+}
+
 // Exact int64 re-score of overflowed lanes: the reference's 64-bit
 // recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
@@ -512,6 +656,25 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     else if (np == 32) hipLaunchKernelGGL((strip_f16m_kernel<32>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
     else hipLaunchKernelGGL((strip_f16m_kernel<16>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
+}
+
+template <int W>
+static hipError_t launch_pair_w(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
+    const uint32_t blocks = (a.ngroups + W - 1) / W;
+    if (blocks == 0) return hipSuccess;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)sw_pair_kernel<16, W>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLdsMax);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((sw_pair_kernel<16, W>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_pair(const StripArgs& a, size_t lds_bytes, int waves, hipStream_t st) {
+    return waves == 4 ? launch_pair_w<4>(a, lds_bytes, st) : launch_pair_w<8>(a, lds_bytes, st);
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
 run() {   # name, rocprof args...
     local name=$1; shift
-    timeout -k 10 300 rocprofv3 "$@" --kernel-include-regex strip16 -d "$OUT/$name" -o run --output-format csv \
+    timeout -k 10 300 rocprofv3 "$@" --kernel-include-regex "strip|pair" -d "$OUT/$name" -o run --output-format csv \
         -- python3 "$REPO/bench.py" $ARGS > "$OUT/$name.log" 2>&1
 }
 run stats --kernel-trace --stats

@@ -45,6 +45,11 @@ INSTRS = {
     "v_maximum3_f32": "v_maximum3_f32 %0, %0, %1, %2",
     "v_dot2_i32_i16": "v_dot2_i32_i16 %0, %1, %2, %0",
     "v_sad_u16": "v_sad_u16 %0, %1, %2, %0",
+    "mix_max3_add": "v_pk_maximum3_f16 %0, %0, %1, %2\\n\\tv_add_u32 %0, %0, %1",
+    "mix_max3_2add": "v_pk_maximum3_f16 %0, %0, %1, %2\\n\\tv_add_u32 %0, %0, %1\\n\\tv_add_u32 %0, %0, %2",
+    "mix_pkadd_max3": "v_pk_add_u16 %0, %0, %1\\n\\tv_pk_maximum3_f16 %0, %0, %1, %2",
+    "v_pk_maximum3_f16x2": "v_pk_maximum3_f16 %0, %0, %1, %2\\n\\tv_pk_maximum3_f16 %0, %0, %2, %1",
+    "v_add_u32x2": "v_add_u32 %0, %0, %1\\n\\tv_add_u32 %0, %0, %2",
 }
 import sys
 only = sys.argv[1:] if len(sys.argv) > 1 else list(INSTRS)
