@@ -30,6 +30,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+# VALU instructions per cell of each scoring kernel, from PMC SQ_INSTS_VALU
+# (64 lanes per instruction) over the C2/C3 launches: profiles/r01/pmc_*
+VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 4.32}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -178,7 +183,7 @@ def main():
     # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
     # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
     # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_c2_sw_np16).
-    instr_per_cell = {("sw", 16): 5.59}.get((args.algo, args.strip_np))
+    instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 else None
     issue_cycles = 4.17
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
@@ -201,7 +206,7 @@ def main():
                    "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "strip_np": args.strip_np},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
-        "kernel": {"name": "strip16_kernel", "avg_ms": round(kavg, 4),
+        "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
                    "wide_ms_avg": round(float(np.mean(wide_ms)), 4),
                    "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,

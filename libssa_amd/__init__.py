@@ -63,7 +63,8 @@ class ssa_amd_stats_t(Structure):
     _fields_ = [("search_ms", c_double), ("kernel_ms", c_double), ("wide_ms", c_double), ("d2h_ms", c_double),
                 ("replay_ms", c_double), ("pack_ms", c_double), ("cells", c_uint64), ("entries", c_uint64),
                 ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
-                ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64)]
+                ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64),
+                ("kernel", ctypes.c_char * 32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -184,7 +185,9 @@ def set_option(name, value): load().ssa_amd_set_option(_b(name), value)
 def stats():
     s = ssa_amd_stats_t()
     load().ssa_amd_get_stats(ctypes.byref(s))
-    return {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
+    d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
+    d["kernel"] = d["kernel"].decode()
+    return d
 
 
 def search(q, algo, hitcount, bit_width=BIT_WIDTH_16, mode=TOPK, cap=None):

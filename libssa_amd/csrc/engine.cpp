@@ -289,6 +289,33 @@ static uint32_t nw_int16_limit(size_t m, int Q, int R, int64_t minM, int64_t max
     return (uint32_t)a;
 }
 
+// NW on f16 bit patterns (pair_kernel<.., NW=true>): values are stored as
+// v + base and every real value and intermediate of an entry of length n must
+// stay inside [0x0400, 0x7BFF].  Upper bound (m+1)*maxM fixes base; the
+// two-gap lower bound then limits n.  Returns the largest admissible n (0 when
+// the query cannot use the f16 path at all) and the base.
+static uint32_t nw_f16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM, uint32_t* base) {
+    *base = 0;
+    if (Q > 0 || R > 0) return 0;
+    const int64_t up = std::max<int64_t>(maxM, 0), lo = std::min<int64_t>(minM, 0);
+    const int64_t U = (int64_t)(m + 1) * up;
+    if (U > 0x77FF - 64) return 0;
+    const int64_t b = 0x7BFF - U;
+    auto ok = [&](uint64_t n) {
+        const int64_t L = 3 * (int64_t)Q + (int64_t)(m + n + 4) * R + lo;
+        return L + b >= 0x0400;
+    };
+    if (!ok(0)) return 0;
+    *base = (uint32_t)b;
+    if (R == 0) return 0xffffffffu;
+    uint64_t a = 0, c = 0xffffffffull;
+    while (c - a > 1) {
+        const uint64_t x = (a + c) / 2;
+        if (ok(x)) a = x; else c = x;
+    }
+    return (uint32_t)a;
+}
+
 void device_search(const std::vector<QueryView>& views, int algo, SearchScores& out) {
     DeviceDB& D = device_db();
     check(hipSetDevice(D.device), "hipSetDevice");
@@ -313,6 +340,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
     uint64_t kernel_bytes = 0;
+    const char* kname = "";
 
     for (size_t v = 0; v < V; v++) {
         const QueryView& qv = views[v];
@@ -341,11 +369,24 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         if (C.force_wide) nmax16 = 0;
         // SW on f16 bit patterns needs non-positive gaps and scores within
         // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
-        const bool use_f16 = !nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024;
-        // pair-symbol profile (sw_pair_kernel): (alpha+1)^2 rows in LDS
         const uint32_t prow = A + 1;
         const size_t pair_lds = (size_t)prow * prow * (np + 4) * 4;
-        const bool use_pair = use_f16 && C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax;
+        // NW on f16 patterns: only when no more than a handful of entries
+        // exceed its length bound (those are re-scored by the int64 kernel)
+        uint32_t nw_base = 0, nmax_f16 = 0;
+        bool use_nwf16 = false;
+        if (nw && C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
+            nmax_f16 = std::min(nw_f16_limit(m, Q, R, minM, maxM, &nw_base), nmax16);
+            if (nmax_f16 > 0) {
+                size_t beyond = 0;
+                for (size_t e = 0; e < E; e++) beyond += D.meta.len[e] > nmax_f16;
+                use_nwf16 = beyond <= 64;
+            }
+        }
+        if (use_nwf16) nmax16 = nmax_f16;
+        const bool use_f16 = (!nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024) || use_nwf16;
+        // pair-symbol profile (pair_kernel): (alpha+1)^2 rows in LDS
+        const bool use_pair = use_f16 && (use_nwf16 || (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax));
 
         // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
         // pair table, dword (s, c1*prow+c0, r) = (QP[c1][s*2np+r], QP[c0][s*2np+np+r])
@@ -422,6 +463,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         a.ovf_cap = (uint32_t)kOvfCap;
         a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
         a.alpha = A;
+        a.nw_base = nw_base;
 
         WideArgs w{};
         w.res = D.d_res;
@@ -439,8 +481,11 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         w.nw = nw ? 1 : 0;
         w.ovf_cap = (uint32_t)kOvfCap;
 
+        kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
+                         : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
+        if (nmax16 == 0) kname = "wide_i64";
         check(hipEventRecord(D.ev[0], st), "event");
-        check(use_pair ? launch_sw_pair(a, pair_lds, C.pair_waves, st)
+        check(use_pair ? launch_pair(a, pair_lds, C.pair_waves, nw, st)
                        : use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st),
               "strip kernel launch");
         check(hipEventRecord(D.ev[1], st), "event");
@@ -482,6 +527,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
     S.kernel_launches = (uint32_t)V;
     S.device = D.device;
     S.kernel_bytes = kernel_bytes;
+    snprintf(S.kernel, sizeof S.kernel, "%s", kname);
 }
 
 }  // namespace ssa

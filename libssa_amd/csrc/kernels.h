@@ -30,6 +30,8 @@ struct StripArgs {
     uint32_t ovf_cap;          // capacity of ovf_list
     uint32_t pad_word;         // profile dword of the padding residue (both halves)
     uint32_t alpha;            // compact alphabet size; code alpha = padding column
+    uint32_t nw_base;          // NW pattern offset of pair_kernel (value + nw_base)
+    uint32_t strip0, strip1;   // pair_kernel: strips [strip0, strip1) of this launch
 };
 
 struct WideArgs {
@@ -50,7 +52,7 @@ struct WideArgs {
 
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
-hipError_t launch_sw_pair(const StripArgs& a, size_t lds_bytes, int waves, hipStream_t st);
+hipError_t launch_pair(const StripArgs& a, size_t lds_bytes, int waves, bool nw, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
 }  // namespace ssa

@@ -198,7 +198,10 @@ strip16_kernel(const StripArgs a) {
                     Fprev = F;
                     // materialize the running maximum every column; otherwise the
                     // compiler defers the max chain and keeps every H alive
+                    // a per-step anchor the scheduler cannot move work across
+                    // (without it NW's schedule grows past 128 VGPRs and spills)
                     if (!NW) asm volatile("" : "+v"(S));
+                    else asm volatile("" : "+v"(Fprev));
                     if (b == 0 && k == 0) {
                         // the high half just processed the virtual column -1:
                         // install the true left boundary for its rows
@@ -419,21 +422,36 @@ strip_f16m_kernel(const StripArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// SW, f16 bit patterns (as strip_f16m_kernel) with a PAIR-SYMBOL profile.
+// SW and NW on f16 bit patterns with a PAIR-SYMBOL profile (the fast path).
+//
+// Values are 16-bit patterns v + base that order like the positive f16
+// numbers they encode (see strip_f16m_kernel): SW uses base = kF16Floor and
+// the local-alignment floor inside E's max3; NW uses base = a.nw_base, chosen
+// on the host so that every real value and intermediate of entries up to
+// a.nmax16 columns stays inside [0x0400, 0x7BFF] -- NW needs
+// no floor and no saturation.  Padding rows/columns may leave that range;
+// nothing real depends on them (dependencies only run down and right, and a
+// borrow only runs from a low half into the high half, whose cell is at the
+// same or a later column and row).
 //
 // The packed profile operand of one column is (QP[d_j][r], QP[d_{j-1}][r+NP]):
-// low half for the current residue, high half for the previous one (the skew).
-// Indexing the LDS table by the residue pair (d_j, d_{j-1}) returns that
-// operand directly -- no v_bfi_b32 per cell and no VGPR copy of the previous
-// row.  The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB
-// alphabet, +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is
-// shared by the workgroup's W waves, so the waves step through the
-// strips together (one barrier per strip; groups of a workgroup are adjacent
-// in the length order, so their strip lengths nearly match).
+// low half for the current residue, high half for the previous one (the
+// skew).  Indexing the LDS table by the residue pair (d_j, d_{j-1}) returns
+// it directly -- no v_bfi_b32 per cell and no VGPR copy of the previous row.
+// The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB alphabet,
+// +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is shared by
+// the workgroup's W waves, so they step through the strips together (one
+// barrier per strip; groups of a workgroup are adjacent in the length order,
+// so their strips take nearly the same time).
+//
+// A launch covers strips [a.strip0, a.strip1).  NW runs its last strip as a
+// separate CAP=true launch: capturing H(m-1, len-1) costs a 16-way select per
+// column, and keeping it in its own instantiation keeps it from raising the
+// register allocation (and spilling) of the code every other strip runs.
 // ---------------------------------------------------------------------------
-template <int NP, int W>
+template <int NP, int W, bool NW, bool CAP>
 __global__ void __launch_bounds__(64 * W, 4)
-sw_pair_kernel(const StripArgs a) {
+pair_kernel(const StripArgs a) {
     constexpr int ROWW = NP + 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
@@ -450,15 +468,25 @@ sw_pair_kernel(const StripArgs a) {
     const uint32_t gl = gg * 64 + lane;
     const uint32_t prow = a.alpha + 1;
     const uint32_t ntab4 = prow * prow * (NP / 4);  // 16-B chunks per strip table
+    const uint32_t len = a.lane_len[gl];
 
     constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;
-    const int QR = a.gap_open + a.gap_extend, R = a.gap_extend;
-    const uint32_t cQR = (uint32_t)(QR * 65536 + QR);
-    const uint32_t cR = (uint32_t)(R * 65536 + R);
+    const int Q = a.gap_open, R = a.gap_extend, QR = Q + R;
+    const int BASE = NW ? (int)a.nw_base : kF16Floor;
+    const uint32_t cQR = (uint32_t)(QR * 65536 + QR);   // "combined" packed constants:
+    const uint32_t cR = (uint32_t)(R * 65536 + R);      // one v_add_u32 updates both halves
+    auto pat = [&](int v) -> uint32_t { return (uint32_t)(v + BASE) & 0xffffu; };
 
     uint32_t S = FL;
+    uint32_t cap = 0;
+    const int R2 = 2 * NP;
+    const int last_strip = (int)a.nstrips - 1;
+    const int rr = (int)a.m - 1 - last_strip * R2;     // strip row of the last query row
+    const int cap_half = rr >= NP ? 1 : 0;
+    const int cap_row = rr - cap_half * NP;
+    const uint32_t cap_col = len - 1 + cap_half;
 
-    for (int s = 0; s < (int)a.nstrips; s++) {
+    for (int s = (int)a.strip0; s < (int)a.strip1; s++) {
         // ---- the whole workgroup stages this strip's pair table
         __syncthreads();
         const uint4* src = (const uint4*)(a.qpt + (size_t)s * prow * prow * NP);
@@ -469,14 +497,27 @@ sw_pair_kernel(const StripArgs a) {
         __syncthreads();
         if (!active) continue;
         const bool first = (s == 0);
+        const bool capture = CAP && s == last_strip;
+        const int i0 = s * R2;
 
+        // ---- left boundary (column -1): SW 0, NW H(i,-1)=Q+(i+1)R, E_in(i,0)=2Q+(i+2)R.
+        // NW, high halves: step 0 runs them over the virtual column -1, and
+        // the initial values make that step produce the true boundary of
+        // rows i0+NP.. by itself: diagonal input H(i,-1) plus the padding
+        // profile 0, E and F at the pattern minimum, so h = H(i,-1) and the
+        // E leaving it is h+Q+R.
         uint32_t H[NP], E[NP];
 #pragma unroll
         for (int r = 0; r < NP; r++) {
-            H[r] = FL;
-            E[r] = FL;
+            H[r] = NW ? pat(Q + (i0 + r + 1) * R) | (pat(Q + (i0 + NP + r + 2) * R) << 16) : FL;
+            E[r] = NW ? pat(2 * Q + (i0 + r + 2) * R) | (0x0400u << 16) : FL;
         }
-        uint32_t hd0 = FL, Fprev = FL;
+        // diagonal input of row i0 at column 0, H(i0-1, -1); high half H(i0+NP, -1)
+        uint32_t hd0 = NW ? pat(first ? 0 : Q + i0 * R) | (pat(Q + (i0 + NP + 1) * R) << 16) : FL;
+        uint32_t Fprev = NW ? 0x0400u : FL;
+        // synthesized top boundary of the first strip: (H(-1,j), F into row 0)
+        uint32_t rbsyn = NW ? (pat(Q + R) | (pat(2 * Q + 2 * R) << 16)) : FL;
+
         uint32_t ob[4] = {0, 0, 0, 0};
         uint4 rnext = resp[0];
         uint4 qnext = first ? make_uint4(0, 0, 0, 0) : rbp[0];
@@ -504,6 +545,7 @@ sw_pair_kernel(const StripArgs a) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int k = t * 4 + u;
+                    const uint32_t j = b * 16 + k;
                     uint32_t P[NP];
 #pragma unroll
                     for (int r = 0; r < NP; r++) P[r] = nxt[r];
@@ -513,7 +555,13 @@ sw_pair_kernel(const StripArgs a) {
                         load_row<NP>(nxt, lds + (dn * prow + dprev) * ROWW);
                         dprev = dn;
                     }
-                    const uint32_t rbv = first ? FL : qw[u];
+                    uint32_t rbv;
+                    if (first) {
+                        rbv = rbsyn;
+                        if (NW) rbsyn += cR;
+                    } else {
+                        rbv = qw[u];
+                    }
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
 #pragma unroll
@@ -522,17 +570,27 @@ sw_pair_kernel(const StripArgs a) {
                         hd = H[r];
                         H[r] = h;
                         const uint32_t tt = h + cQR;
-                        E[r] = fmax3(E[r] + cR, tt, FL);
+                        E[r] = NW ? fmax2(E[r] + cR, tt) : fmax3(E[r] + cR, tt, FL);
                         F = fmax2(F + cR, tt);
-                        if (r & 1) S = fmax3(S, H[r - 1], H[r]);
+                        if (!NW && (r & 1)) S = fmax3(S, H[r - 1], H[r]);
                     }
                     hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
                     Fprev = F;
-                    asm volatile("" : "+v"(S));
-                    if (!(b == 0 && k == 0)) {
+                    // a per-step anchor the scheduler cannot move work across
+                    // (without it NW's schedule grows past 128 VGPRs and spills)
+                    if (!NW) asm volatile("" : "+v"(S));
+                    else asm volatile("" : "+v"(Fprev));
+                    // step 0's high half is the virtual column -1: no output
+                    if (b != 0 || k != 0) {
                         ob[(k + 3) & 3] = perm(F, H[NP - 1], SEL_LO_BHI_HI_AHI);
                         if ((k & 3) == 0)
                             rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                    }
+                    if (capture) {
+                        uint32_t hsel = H[0];
+#pragma unroll
+                        for (int r = 1; r < NP; r++) hsel = (cap_row == r) ? H[r] : hsel;
+                        cap = (j == cap_col) ? hsel : cap;
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -542,23 +600,29 @@ sw_pair_kernel(const StripArgs a) {
         rbp[(size_t)(nblk * 4 - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
     }
 
-    if (!active) return;
-    const uint32_t len = a.lane_len[gl];
+    if (!active || a.strip1 != a.nstrips) return;
     const uint32_t o = a.lane_out[gl];
     if (o == 0xffffffffu) return;
     if (len == 0) {
-        a.scores[o] = 0;
+        a.scores[o] = NW ? (int32_t)(a.gap_open + (int64_t)a.m * a.gap_extend) : 0;
         return;
     }
-    const uint32_t slo = S & 0xffffu, shi = S >> 16;
-    const uint32_t smax = slo > shi ? slo : shi;
-    const bool ovf = smax >= 0x7C00u || len > a.nmax16;
+    int32_t score;
+    bool ovf = len > a.nmax16;
+    if (!NW) {
+        const uint32_t slo = S & 0xffffu, shi = S >> 16;
+        const uint32_t smax = slo > shi ? slo : shi;
+        ovf = ovf || smax >= 0x7C00u;
+        score = (int32_t)smax - kF16Floor;
+    } else {
+        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE;
+    }
     if (ovf) {
         const uint32_t idx = atomicAdd(a.ovf_count, 1u);
         if (idx < a.ovf_cap) a.ovf_list[idx] = gl;
         a.scores[o] = INT32_MIN;
     } else {
-        a.scores[o] = (int32_t)smax - kF16Floor;
+        a.scores[o] = score;
     }
 }
 
@@ -658,23 +722,39 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int W>
+template <int W, bool NW, bool CAP>
 static hipError_t launch_pair_w(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
     const uint32_t blocks = (a.ngroups + W - 1) / W;
-    if (blocks == 0) return hipSuccess;
+    if (blocks == 0 || a.strip0 >= a.strip1) return hipSuccess;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)sw_pair_kernel<16, W>,
+        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<16, W, NW, CAP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLdsMax);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((sw_pair_kernel<16, W>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
+    hipLaunchKernelGGL((pair_kernel<16, W, NW, CAP>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_sw_pair(const StripArgs& a, size_t lds_bytes, int waves, hipStream_t st) {
-    return waves == 4 ? launch_pair_w<4>(a, lds_bytes, st) : launch_pair_w<8>(a, lds_bytes, st);
+template <int W>
+static hipError_t launch_pair_waves(const StripArgs& a, size_t lds_bytes, bool nw, hipStream_t st) {
+    StripArgs b = a;
+    b.strip0 = 0;
+    b.strip1 = a.nstrips;
+    if (!nw) return launch_pair_w<W, false, false>(b, lds_bytes, st);
+    // NW: every strip but the last, then the last one with the capture of
+    // the final row (its own instantiation, see pair_kernel)
+    b.strip1 = a.nstrips - 1;
+    hipError_t e = launch_pair_w<W, true, false>(b, lds_bytes, st);
+    if (e != hipSuccess) return e;
+    b.strip0 = a.nstrips - 1;
+    b.strip1 = a.nstrips;
+    return launch_pair_w<W, true, true>(b, lds_bytes, st);
+}
+
+hipError_t launch_pair(const StripArgs& a, size_t lds_bytes, int waves, bool nw, hipStream_t st) {
+    return waves == 4 ? launch_pair_waves<4>(a, lds_bytes, nw, st) : launch_pair_waves<8>(a, lds_bytes, nw, st);
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

@@ -132,7 +132,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
-        for swk in ((0, 1) if algo == S.SW else (0,)):
+        for swk in (0, 1):
             S.set_option("sw_kernel", swk)
             for np_ in (8, 16, 32):
                 S.set_option("strip_np", np_)
@@ -164,6 +164,35 @@ def test_sw_f16_pattern_limit(match):
             S.set_option("sw_kernel", swk)
             sc, _ = _full_scores(qq, S.SW, len(seqs))
             assert (sc == exp).all(), (swk, sc, exp)
+        S.set_option("sw_kernel", 0)
+        S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("n_long", [5, 200])
+def test_nw_f16_length_bound(n_long):
+    """NW on f16 patterns admits entries up to a length bound derived from the
+    query, matrix and gaps (engine.cpp nw_f16_limit): with R=-30 and a
+    100-residue query it is 874, the int16 bound 984.  Lengths straddle both;
+    a few long entries are re-scored exactly, many long ones switch the whole
+    search to the int16 kernel -- every score stays exact either way."""
+    rng = np.random.default_rng(n_long)
+    q = syn.protein_query(100, 11)
+    lens = np.concatenate([np.arange(860, 890), [980, 984, 985, 990, 1200],
+                           rng.integers(860, 1000, n_long), rng.integers(1, 400, 300)]).astype(np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    exp = po.scores(S.NW, q, codes, off, M, -40, -30)
+    configure(False, ("builtin", "blosum62"), -40, -30)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for swk in (0, 1):
+            S.set_option("sw_kernel", swk)
+            sc, _ = _full_scores(qq, S.NW, len(lens))
+            assert (sc == exp).all(), (swk, np.nonzero(sc != exp)[0][:10])
+            assert S.stats()["wide_count"] >= 2
         S.set_option("sw_kernel", 0)
         S.free_sequence(qq)
 

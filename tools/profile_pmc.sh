@@ -23,4 +23,5 @@ run write --kernel-trace --pmc WRITE_SIZE
 run valu --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 run wait --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
 run lds --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE
+run icache --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_INSTS_SMEM
 echo "profiles in $OUT"
