@@ -31,8 +31,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 # VALU instructions per cell of each scoring kernel, from PMC SQ_INSTS_VALU
-# (64 lanes per instruction) over the C2/C3 launches: profiles/r01/pmc_*
-VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 4.32}
+# (64 lanes per instruction) over the C2 (SW) / C3 (NW) launches:
+# profiles/r01/pmc_c2_sw_np16 (strip16), pmc_c2_pair, pmc_c3_pair
+VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 4.33, "pair_f16_nw": 4.08}
 
 
 def parse():

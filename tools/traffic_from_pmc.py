@@ -12,21 +12,22 @@ import os
 import sys
 
 
-def mean_counter(d, name):
+def mean_counter(d, name, kernel=None):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
-            if r["Counter_Name"] == name]
+            if r["Counter_Name"] == name and (kernel is None or kernel in r["Kernel_Name"])]
     return sum(vals) / len(vals)
 
 
 def main():
     pmc_dir, key = sys.argv[1], sys.argv[2]
-    fetch = mean_counter(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE") * 1024 * 2
-    write = mean_counter(os.path.join(pmc_dir, "write"), "WRITE_SIZE") * 1024
+    kernel = sys.argv[3] if len(sys.argv) > 3 else None   # substring of the dominant kernel's name
+    fetch = mean_counter(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE", kernel) * 1024 * 2
+    write = mean_counter(os.path.join(pmc_dir, "write"), "WRITE_SIZE", kernel) * 1024
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "profiles", "traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[key] = {"bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
-                 "source": os.path.relpath(pmc_dir, root)}
+                 "source": os.path.relpath(pmc_dir, root), "kernel": kernel}
     json.dump(data, open(path, "w"), indent=1)
     print(key, data[key])
 
