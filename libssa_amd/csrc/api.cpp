@@ -285,7 +285,6 @@ void ssa_amd_set_option(const char* name, long value) {
     if (!strcmp(name, "strip_np")) cfg().strip_np = (int)value;
     else if (!strcmp(name, "force_wide")) cfg().force_wide = (int)value;
     else if (!strcmp(name, "sw_kernel")) cfg().sw_kernel = (int)value;
-    else if (!strcmp(name, "pair_waves")) cfg().pair_waves = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -32,7 +32,6 @@ struct Config {
     int strip_np = 16;                    // packed rows per strip (2*np query rows)
     int waves_per_block = 4;
     int force_wide = 0;                   // 1: score everything with the int64 kernel
-    int pair_waves = 4;                   // waves per workgroup sharing one pair table (4 or 8)
     int sw_kernel = 0;                    // 0: f16-pattern kernel when applicable, 1: int16 kernel
 };
 Config& cfg();

@@ -42,13 +42,13 @@ void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
-    dfree(d_work);
+    dfree(d_work); dfree(d_smax);
     if (h_scores) (void)hipHostFree(h_scores);
     if (h_ovf) (void)hipHostFree(h_ovf);
     if (h_wide) (void)hipHostFree(h_wide);
     d_groups = nullptr; d_res = nullptr; d_rowbuf = nullptr; d_lane_len = nullptr; d_lane_out = nullptr;
     d_scores = nullptr; d_ovf = nullptr; d_wide = nullptr; d_qpt = nullptr; d_query = nullptr;
-    d_matrix = nullptr; d_work = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
+    d_matrix = nullptr; d_work = nullptr; d_smax = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
     h_scores_cap = qpt_cap = query_cap = work_cap = 0;
     generation = ~0ull;
     meta = EntryMeta();
@@ -189,10 +189,12 @@ void ensure_device_db() {
     uint64_t blocks = 0;
     for (uint32_t g = 0; g < ngroups; g++) {
         const uint32_t longest = S.meta.len[order[(size_t)g * 64]];
-        const uint32_t ncols = ((longest + 1) + 15) / 16 * 16;
+        // columns to compute: longest + 1 (the high half lags one column),
+        // rounded to the 4-column row-buffer quad; residues in 16-column blocks
+        const uint32_t ncols = ((longest + 1) + 3) / 4 * 4;
         groups[g].blk = (uint32_t)blocks;
         groups[g].ncols = ncols;
-        blocks += ncols / 16;
+        blocks += (ncols + 15) / 16;
     }
     if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
     // compact alphabet: the residue codes that occur, in code order; the
@@ -243,6 +245,7 @@ void ensure_device_db() {
     dalloc((void**)&D.d_rowbuf, res.size() * 4, "row buffer");
     dalloc((void**)&D.d_lane_len, lane_len.size() * 4, "lane_len");
     dalloc((void**)&D.d_lane_out, lane_out.size() * 4, "lane_out");
+    dalloc((void**)&D.d_smax, lane_out.size() * 4, "running max");
     dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
     dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
     dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
@@ -389,7 +392,8 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         const bool use_pair = use_f16 && (use_nwf16 || (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax));
 
         // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
-        // pair table, dword (s, c1*prow+c0, r) = (QP[c1][s*2np+r], QP[c0][s*2np+np+r])
+        // pair table of a strip of height 2P from row i0,
+        //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
         const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
         auto val = [&](uint32_t c, size_t i) -> int16_t {
@@ -397,17 +401,36 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
             const int64_t x = M[(D.code_of[c] << 5) + qv.seq[i]];
             return (int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, x));
         };
+        struct PairLaunch { int np; uint32_t row0, nstrips; size_t qoff; uint32_t flags; bool cap; };
+        std::vector<PairLaunch> plan;
         std::vector<uint32_t> qpt;
         if (use_pair) {
-            qpt.resize((size_t)nstrips * prow * prow * np);
-            for (uint32_t s = 0; s < nstrips; s++)
-                for (uint32_t c1 = 0; c1 < prow; c1++)
-                    for (uint32_t c0 = 0; c0 < prow; c0++)
-                        for (int r = 0; r < np; r++) {
-                            const size_t i = (size_t)s * 2 * np + r;
-                            qpt[(((size_t)s * prow + c1) * prow + c0) * np + r] =
-                                (uint32_t)(uint16_t)val(c1, i) | ((uint32_t)(uint16_t)val(c0, i + np) << 16);
-                        }
+            // 32-row strips; a remainder of <= 16 rows becomes one 16-row
+            // (NP = 8) strip; NW's last strip runs as its own capture launch
+            const uint32_t full = (uint32_t)(m / 32), rem = (uint32_t)(m % 32);
+            const bool tail = rem > 0 && rem <= 16;
+            const uint32_t nmain = tail || rem == 0 ? full : full + 1;
+            auto add_tables = [&](int P, uint32_t row0, uint32_t count) {
+                const size_t off = qpt.size();
+                qpt.resize(off + (size_t)count * prow * prow * P);
+                for (uint32_t s = 0; s < count; s++)
+                    for (uint32_t c1 = 0; c1 < prow; c1++)
+                        for (uint32_t c0 = 0; c0 < prow; c0++)
+                            for (int r = 0; r < P; r++) {
+                                const size_t i = row0 + (size_t)s * 2 * P + r;
+                                qpt[off + (((size_t)s * prow + c1) * prow + c0) * P + r] =
+                                    (uint32_t)(uint16_t)val(c1, i) | ((uint32_t)(uint16_t)val(c0, i + P) << 16);
+                            }
+                return off;
+            };
+            const uint32_t nbulk = nw && !tail ? nmain - 1 : nmain;
+            if (nbulk > 0) plan.push_back({16, 0, nbulk, add_tables(16, 0, nbulk), 0, false});
+            if (tail) plan.push_back({8, full * 32, 1, add_tables(8, full * 32, 1), 0, nw});
+            else if (nw) plan.push_back({16, nbulk * 32, 1, add_tables(16, nbulk * 32, 1), 0, true});
+            for (size_t l = 0; l < plan.size(); l++) {
+                if (l > 0) plan[l].flags |= kPairCarryIn;
+                if (l + 1 == plan.size()) plan[l].flags |= kPairFinal;
+            }
         } else {
             qpt.resize((size_t)nstrips * 32 * np);
             for (uint32_t s = 0; s < nstrips; s++)
@@ -464,6 +487,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
         a.alpha = A;
         a.nw_base = nw_base;
+        a.smax = D.d_smax;
 
         WideArgs w{};
         w.res = D.d_res;
@@ -485,9 +509,18 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
         check(hipEventRecord(D.ev[0], st), "event");
-        check(use_pair ? launch_pair(a, pair_lds, C.pair_waves, nw, st)
-                       : use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st),
-              "strip kernel launch");
+        if (use_pair) {
+            for (const PairLaunch& l : plan) {
+                StripArgs b = a;
+                b.qpt = D.d_qpt + l.qoff;
+                b.row0 = l.row0;
+                b.nstrips = l.nstrips;
+                b.flags = l.flags;
+                check(launch_pair(b, l.np, nw, l.cap, (size_t)prow * prow * (l.np + 4) * 4, st), "pair kernel launch");
+            }
+        } else {
+            check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
+        }
         check(hipEventRecord(D.ev[1], st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         check(hipEventRecord(D.ev[2], st), "event");

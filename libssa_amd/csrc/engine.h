@@ -37,6 +37,7 @@ struct DeviceDB {
     uint4* d_rowbuf = nullptr;
     uint32_t* d_lane_len = nullptr;
     uint32_t* d_lane_out = nullptr;
+    uint32_t* d_smax = nullptr;           // SW running max between pair_kernel launches
     int32_t* d_scores = nullptr;
     int32_t* h_scores = nullptr;          // pinned, [views][entries]
     size_t h_scores_cap = 0;

@@ -6,12 +6,13 @@
 namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
-constexpr size_t kPairLdsMax = 80 * 1024;   // pair table budget: two workgroups per CU
+constexpr int kPairWaves = 4;      // waves per pair_kernel workgroup (they share one pair table)
+constexpr size_t kPairLdsMax = 80 * 1024;   // pair table budget (35 KiB for proteins: 4 workgroups per CU)
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
 struct GroupDesc {
     uint32_t blk;     // residue offset in 1 KiB blocks (16 columns x 64 lanes)
-    uint32_t ncols;   // padded column count, multiple of 16, >= longest + 1
+    uint32_t ncols;   // columns to compute: multiple of 4, >= longest + 1 (blocks: ceil(ncols/16))
 };
 
 struct StripArgs {
@@ -31,8 +32,14 @@ struct StripArgs {
     uint32_t pad_word;         // profile dword of the padding residue (both halves)
     uint32_t alpha;            // compact alphabet size; code alpha = padding column
     uint32_t nw_base;          // NW pattern offset of pair_kernel (value + nw_base)
-    uint32_t strip0, strip1;   // pair_kernel: strips [strip0, strip1) of this launch
+    // pair_kernel launches (engine.cpp plans them): a.nstrips strips from
+    // query row row0, tables at qpt; flags below; SW running max carried in smax
+    uint32_t row0;
+    uint32_t flags;
+    uint32_t* smax;            // [ngroups * 64]
 };
+constexpr uint32_t kPairFinal = 1;      // this launch holds the query's last row: write scores
+constexpr uint32_t kPairCarryIn = 2;    // SW: start from the running max in smax
 
 struct WideArgs {
     const uint4* res;
@@ -52,7 +59,7 @@ struct WideArgs {
 
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
-hipError_t launch_pair(const StripArgs& a, size_t lds_bytes, int waves, bool nw, hipStream_t st);
+hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
 }  // namespace ssa

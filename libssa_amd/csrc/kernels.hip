@@ -77,7 +77,7 @@ strip16_kernel(const StripArgs a) {
 
     uint32_t* lds = lds_all[wave];
     const GroupDesc gd = a.groups[g];
-    const uint32_t nblk = gd.ncols >> 4;
+    const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
     uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
     const uint32_t gl = g * 64 + lane;
@@ -310,7 +310,7 @@ strip_f16m_kernel(const StripArgs a) {
 
     uint32_t* lds = lds_all[wave];
     const GroupDesc gd = a.groups[g];
-    const uint32_t nblk = gd.ncols >> 4;
+    const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
     uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
     const uint32_t gl = g * 64 + lane;
@@ -428,7 +428,7 @@ strip_f16m_kernel(const StripArgs a) {
 // numbers they encode (see strip_f16m_kernel): SW uses base = kF16Floor and
 // the local-alignment floor inside E's max3; NW uses base = a.nw_base, chosen
 // on the host so that every real value and intermediate of entries up to
-// a.nmax16 columns stays inside [0x0400, 0x7BFF] (DESIGN.md §3.3) -- NW needs
+// a.nmax16 columns stays inside [0x0400, 0x7BFF] (DESIGN.md §3.4) -- NW needs
 // no floor and no saturation.  Padding rows/columns may leave that range;
 // nothing real depends on them (dependencies only run down and right, and a
 // borrow only runs from a low half into the high half, whose cell is at the
@@ -440,18 +440,27 @@ strip_f16m_kernel(const StripArgs a) {
 // it directly -- no v_bfi_b32 per cell and no VGPR copy of the previous row.
 // The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB alphabet,
 // +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is shared by
-// the workgroup's W waves, so they step through the strips together (one
+// the workgroup's waves, so they step through the strips together (one
 // barrier per strip; groups of a workgroup are adjacent in the length order,
 // so their strips take nearly the same time).
 //
-// A launch covers strips [a.strip0, a.strip1).  NW runs its last strip as a
-// separate CAP=true launch: capturing H(m-1, len-1) costs a 16-way select per
-// column, and keeping it in its own instantiation keeps it from raising the
-// register allocation (and spilling) of the code every other strip runs.
+// One launch covers a.nstrips strips starting at query row a.row0 (the host
+// plans the launches, engine.cpp): the bulk of the query in 32-row strips
+// (NP = 16), a remainder of <= 16 rows as one NP = 8 strip instead of a
+// half-empty 32-row one, and for NW the last strip in its own CAP launch:
+// capturing H(m-1, len-1) costs a 16-way select per column, and in the same
+// instantiation it raised the register allocation of the code every other
+// strip runs (past 128 VGPRs: spills).  SW carries its running maximum from
+// one launch to the next through a.smax.
+//
+// Columns are processed up to GroupDesc::ncols (a multiple of 4, >= the
+// group's longest entry + 1) in 16-column residue blocks with a uniform exit
+// inside the last block.
 // ---------------------------------------------------------------------------
-template <int NP, int W, bool NW, bool CAP>
-__global__ void __launch_bounds__(64 * W, 4)
+template <int NP, bool NW, bool CAP>
+__global__ void __launch_bounds__(64 * kPairWaves, 4)
 pair_kernel(const StripArgs a) {
+    constexpr int W = kPairWaves;
     constexpr int ROWW = NP + 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
@@ -462,7 +471,8 @@ pair_kernel(const StripArgs a) {
     const uint32_t gg = active ? g : 0;
 
     const GroupDesc gd = a.groups[gg];
-    const uint32_t nblk = gd.ncols >> 4;
+    const uint32_t nquads = gd.ncols >> 2;
+    const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
     uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
     const uint32_t gl = gg * 64 + lane;
@@ -478,15 +488,16 @@ pair_kernel(const StripArgs a) {
     auto pat = [&](int v) -> uint32_t { return (uint32_t)(v + BASE) & 0xffffu; };
 
     uint32_t S = FL;
+    if (!NW && (a.flags & kPairCarryIn) && active) S = a.smax[gl];
     uint32_t cap = 0;
     const int R2 = 2 * NP;
-    const int last_strip = (int)a.nstrips - 1;
-    const int rr = (int)a.m - 1 - last_strip * R2;     // strip row of the last query row
+    const int last = (int)a.nstrips - 1;
+    const int rr = (int)a.m - 1 - ((int)a.row0 + last * R2);   // strip row of the last query row
     const int cap_half = rr >= NP ? 1 : 0;
     const int cap_row = rr - cap_half * NP;
     const uint32_t cap_col = len - 1 + cap_half;
 
-    for (int s = (int)a.strip0; s < (int)a.strip1; s++) {
+    for (int s = 0; s < (int)a.nstrips; s++) {
         // ---- the whole workgroup stages this strip's pair table
         __syncthreads();
         const uint4* src = (const uint4*)(a.qpt + (size_t)s * prow * prow * NP);
@@ -496,9 +507,9 @@ pair_kernel(const StripArgs a) {
         }
         __syncthreads();
         if (!active) continue;
-        const bool first = (s == 0);
-        const bool capture = CAP && s == last_strip;
-        const int i0 = s * R2;
+        const int i0 = (int)a.row0 + s * R2;    // first query row of the strip
+        const bool first = (i0 == 0);
+        const bool capture = CAP && s == last;
 
         // ---- left boundary (column -1): SW 0, NW H(i,-1)=Q+(i+1)R, E_in(i,0)=2Q+(i+2)R.
         // NW, high halves: step 0 runs them over the virtual column -1, and
@@ -536,10 +547,11 @@ pair_kernel(const StripArgs a) {
             const uint32_t rw[4] = {rcur.x, rcur.y, rcur.z, rcur.w};
 #pragma unroll
             for (int t = 0; t < 4; t++) {
+                if (b * 4 + t >= nquads) break;      // uniform: the group's last columns
                 const uint4 qcur = qnext;
                 if (!first) {
                     const uint32_t nq = b * 4 + t + 1;
-                    if (nq < nblk * 4) qnext = rbp[(size_t)nq * 64];
+                    if (nq < nquads) qnext = rbp[(size_t)nq * 64];
                 }
                 const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
 #pragma unroll
@@ -597,10 +609,14 @@ pair_kernel(const StripArgs a) {
             }
         }
         ob[3] = FL;
-        rbp[(size_t)(nblk * 4 - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
     }
 
-    if (!active || a.strip1 != a.nstrips) return;
+    if (!active) return;
+    if (!(a.flags & kPairFinal)) {
+        if (!NW) a.smax[gl] = S;
+        return;
+    }
     const uint32_t o = a.lane_out[gl];
     if (o == 0xffffffffu) return;
     if (len == 0) {
@@ -722,39 +738,28 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int W, bool NW, bool CAP>
-static hipError_t launch_pair_w(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
-    const uint32_t blocks = (a.ngroups + W - 1) / W;
-    if (blocks == 0 || a.strip0 >= a.strip1) return hipSuccess;
+template <int NP, bool NW, bool CAP>
+static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<16, W, NW, CAP>,
+        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<NP, NW, CAP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLdsMax);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pair_kernel<16, W, NW, CAP>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
+    const uint32_t blocks = (a.ngroups + kPairWaves - 1) / kPairWaves;
+    hipLaunchKernelGGL((pair_kernel<NP, NW, CAP>), dim3(blocks), dim3(64 * kPairWaves), lds_bytes, st, a);
     return hipGetLastError();
 }
 
-template <int W>
-static hipError_t launch_pair_waves(const StripArgs& a, size_t lds_bytes, bool nw, hipStream_t st) {
-    StripArgs b = a;
-    b.strip0 = 0;
-    b.strip1 = a.nstrips;
-    if (!nw) return launch_pair_w<W, false, false>(b, lds_bytes, st);
-    // NW: every strip but the last, then the last one with the capture of
-    // the final row (its own instantiation, see pair_kernel)
-    b.strip1 = a.nstrips - 1;
-    hipError_t e = launch_pair_w<W, true, false>(b, lds_bytes, st);
-    if (e != hipSuccess) return e;
-    b.strip0 = a.nstrips - 1;
-    b.strip1 = a.nstrips;
-    return launch_pair_w<W, true, true>(b, lds_bytes, st);
-}
-
-hipError_t launch_pair(const StripArgs& a, size_t lds_bytes, int waves, bool nw, hipStream_t st) {
-    return waves == 4 ? launch_pair_waves<4>(a, lds_bytes, nw, st) : launch_pair_waves<8>(a, lds_bytes, nw, st);
+hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st) {
+    if (a.ngroups == 0 || a.nstrips == 0) return hipSuccess;
+    if (np == 8) {
+        if (!nw) return launch_pair_t<8, false, false>(a, lds_bytes, st);
+        return cap ? launch_pair_t<8, true, true>(a, lds_bytes, st) : launch_pair_t<8, true, false>(a, lds_bytes, st);
+    }
+    if (!nw) return launch_pair_t<16, false, false>(a, lds_bytes, st);
+    return cap ? launch_pair_t<16, true, true>(a, lds_bytes, st) : launch_pair_t<16, true, false>(a, lds_bytes, st);
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

@@ -114,7 +114,7 @@ def test_random_golden_full_score_vectors(fname):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100])
+@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 48, 49, 63, 64, 65, 100])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_query_length_edges_vs_oracle(qlen, algo):
     rng = np.random.default_rng(qlen)
