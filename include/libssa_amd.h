@@ -76,6 +76,29 @@ size_t ssa_amd_search( p_query query, int algo, size_t hitcount, int bit_width, 
  * writes the sorted top-k (score desc, id desc).  Returns the count. */
 size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );
 
+/* COMPUTE_ALIGNMENT traceback of one (query, DB sequence) pair of mapped
+ * codes with the current matrix and gap penalties (reference align.c +
+ * cigar.c, the same routine sw_align/nw_align use for their hits).  Writes
+ * region = {query begin, query end, db begin, db end} and the NUL-terminated
+ * CIGAR (truncated to cap - 1 characters); returns the CIGAR length. */
+size_t ssa_amd_align_pair( int algo, const char * query, size_t qlen, const char * db, size_t dlen,
+                           size_t region[4], char * cigar, size_t cap );
+
+/* The query buffers a search scores for the current symbol type and strands
+ * (reference searcher.c:42-90): one q_seq_t per strand/frame view, codes as
+ * handed out in alignment_t.query.seq.  Writes up to cap views; returns the
+ * number of views. */
+size_t ssa_amd_query_views( p_query query, q_seq_t * out, size_t cap );
+
+/* Translates mapped nucleotide codes (map_ncbi_nt16 values) with the query
+ * (db_side = 0) or DB (db_side = 1) genetic code chosen by
+ * init_symbol_translation, strand 0 (forward) or 1 (reverse complement),
+ * frame 0..2 -- reference util_sequence.c:332-382.  Writes min(result, cap)
+ * amino-acid codes; returns the protein length (len - frame) / 3, 0 when
+ * len < frame. */
+size_t ssa_amd_translate( int db_side, const char * nt_codes, size_t len, int strand, int frame,
+                          char * out, size_t cap );
+
 #ifdef __cplusplus
 }
 #endif

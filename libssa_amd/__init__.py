@@ -78,7 +78,7 @@ EXPORTS = {
                       "init_db", "init_sequence_fasta", "free_sequence", "sw_align", "nw_align", "free_alignment",
                       "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
                       "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
-                      "ssa_amd_replay"],
+                      "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -111,6 +111,10 @@ def load():
         "ssa_amd_get_stats": ([POINTER(ssa_amd_stats_t)], None), "ssa_amd_set_option": ([c_char_p, c_long], None),
         "ssa_amd_search": ([P, c_int, c_size_t, c_int, c_int, POINTER(ssa_hit_t), c_size_t], c_size_t),
         "ssa_amd_replay": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
+        "ssa_amd_query_views": ([P, POINTER(q_seq_t), c_size_t], c_size_t),
+        "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
+                               c_size_t),
+        "ssa_amd_translate": ([c_int, c_char_p, c_size_t, c_int, c_int, c_char_p, c_size_t], c_size_t),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -151,7 +155,8 @@ def _unpack(alist):
                     "db_strand": x.db_seq.strand, "db_frame": x.db_seq.frame,
                     "q_len": int(x.query.len), "q_strand": x.query.strand, "q_frame": x.query.frame,
                     "db_seq": ctypes.string_at(x.db_seq.seq, x.db_seq.len) if x.db_seq.seq else b"",
-                    "alignment": x.alignment.decode() if x.alignment else None})
+                    "alignment": x.alignment.decode() if x.alignment else None,
+                    "region": (int(x.align_q_start), int(x.align_q_end), int(x.align_d_start), int(x.align_d_end))})
     return out
 
 
@@ -213,3 +218,31 @@ def replay(log, hitcount):
     out = (ssa_hit_t * max(hitcount, 1))()
     c = L.ssa_amd_replay(arr, n, hitcount, out)
     return [(out[i].score, out[i].db_id) for i in range(c)]
+
+
+def query_views(q):
+    """ssa_amd_query_views: [(codes: bytes, strand, frame)] of the search's query buffers."""
+    L = load()
+    buf = (q_seq_t * 8)()
+    n = L.ssa_amd_query_views(q, buf, 8)
+    return [(ctypes.string_at(buf[i].seq, buf[i].len), buf[i].strand, buf[i].frame) for i in range(min(n, 8))]
+
+
+def translate(db_side, nt_codes, strand, frame):
+    """ssa_amd_translate on mapped nucleotide codes; returns amino-acid codes (bytes)."""
+    L = load()
+    src = bytes(nt_codes)
+    out = ctypes.create_string_buffer(len(src) // 3 + 1)
+    n = L.ssa_amd_translate(db_side, src, len(src), strand, frame, out, len(out))
+    return out.raw[:n]
+
+
+def align_pair(algo, query_codes, db_codes):
+    """ssa_amd_align_pair: ((q_begin, q_end, d_begin, d_end), cigar) of one pair."""
+    L = load()
+    q, d = bytes(query_codes), bytes(db_codes)
+    reg = (c_size_t * 4)()
+    n = L.ssa_amd_align_pair(algo, q, len(q), d, len(d), reg, None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    L.ssa_amd_align_pair(algo, q, len(q), d, len(d), reg, buf, n + 1)
+    return tuple(reg), buf.value.decode()

@@ -160,14 +160,11 @@ p_alignment_list build_list(const SearchResult& R) {
 
 p_alignment_list align(p_query q, size_t k, int bw, int at, int algo) {
     test_configuration(q);
-    if (at == COMPUTE_ALIGNMENT) {
-        static bool warned = false;
-        if (!warned) print_warning("COMPUTE_ALIGNMENT: traceback is not implemented yet; returning scores only");
-        warned = true;
-    }
     SearchResult R;
     run_search(q, algo, k, bw, false, R);
-    return build_list(R);
+    p_alignment_list L = build_list(R);
+    if (at == COMPUTE_ALIGNMENT) compute_alignments(L, algo);   // align.cpp (aligner.c:163-181)
+    return L;
 }
 
 }  // namespace
@@ -278,6 +275,39 @@ int ssa_amd_prepare_db(void) {
 
 void ssa_amd_get_stats(ssa_amd_stats_t* out) {
     if (out) *out = stats();
+}
+
+size_t ssa_amd_align_pair(int algo, const char* query, size_t qlen, const char* db, size_t dlen, size_t region[4],
+                          char* cigar, size_t cap) {
+    if (!matrix().ready) fatal("Scoring matrix not initialized");
+    if (algo != SSA_AMD_SW && algo != SSA_AMD_NW) fatal("ssa_amd_align_pair: unknown algorithm %d", algo);
+    size_t rg[4];
+    const std::string c = traceback(algo == SSA_AMD_SW ? kAlgoSW : kAlgoNW, (const uint8_t*)query, qlen,
+                                    (const uint8_t*)db, dlen, rg);
+    if (region) memcpy(region, rg, sizeof rg);
+    if (cigar && cap) {
+        const size_t n = std::min(c.size(), cap - 1);
+        memcpy(cigar, c.data(), n);
+        cigar[n] = 0;
+    }
+    return c.size();
+}
+
+size_t ssa_amd_query_views(p_query query, q_seq_t* out, size_t cap) {
+    if (!query) return 0;
+    const std::vector<QueryView> v = query_views(query);
+    for (size_t i = 0; i < v.size() && i < cap; i++)
+        out[i] = q_seq_t{v[i].cseq, v[i].len, v[i].strand, v[i].frame};
+    return v.size();
+}
+
+size_t ssa_amd_translate(int db_side, const char* nt_codes, size_t len, int strand, int frame, char* out,
+                         size_t cap) {
+    if (frame < 0 || frame > 2 || strand < 0 || strand > 1) fatal("ssa_amd_translate: bad strand/frame");
+    const std::vector<uint8_t> p = translate(db_side != 0, (const uint8_t*)nt_codes, len, strand, frame);
+    const size_t n = p.size() - 1;
+    if (out) memcpy(out, p.data(), std::min(n, cap));
+    return n;
 }
 
 void ssa_amd_set_option(const char* name, long value) {

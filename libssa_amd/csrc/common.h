@@ -113,4 +113,9 @@ private:
 };
 void sort_hits(std::vector<Hit>& v);   // score desc, id desc (util.h:12)
 
+// ------------------------------------------------------ COMPUTE_ALIGNMENT
+// align.cpp: region {q begin, q end, db begin, db end} and CIGAR of a pair
+std::string traceback(int algo, const uint8_t* q, size_t qn, const uint8_t* d, size_t dn, size_t region[4]);
+void compute_alignments(p_alignment_list L, int algo);
+
 }  // namespace ssa

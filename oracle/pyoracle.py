@@ -187,7 +187,8 @@ def have_ref() -> bool:
     return os.path.exists(REF_HARNESS)
 
 
-MODE_SCORES, MODE_SEARCH64, MODE_SEARCH16_AVX2, MODE_SEARCH16_SSE2, MODE_TABLES = 0, 1, 2, 3, 4
+MODE_SCORES, MODE_SEARCH64, MODE_SEARCH16_AVX2, MODE_SEARCH16_SSE2, MODE_TABLES, MODE_TRANSLATE = 0, 1, 2, 3, 4, 5
+MODE_ALIGN = 6
 
 
 def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_open: int = 0,
@@ -222,6 +223,27 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
         data = open(rsp, "rb").read()
     if mode == MODE_SCORES:
         return np.frombuffer(data, dtype=np.int64).copy()
+    if mode == MODE_ALIGN:
+        # per sequence: (q_begin, q_end, d_begin, d_end), cigar
+        out, pos = [], 0
+        for _ in range(nseq):
+            v = struct.unpack_from("<5Q", data, pos)
+            out.append((v[:4], data[pos + 40: pos + 40 + v[4]].decode()))
+            pos += 40 + v[4]
+        return out
+    if mode == MODE_TRANSLATE:
+        # per sequence: side 0/1 x strand 0/1 x frame 0..2, each u64 len + codes
+        out, pos = [], 0
+        for _ in range(nseq):
+            per = {}
+            for side in range(2):
+                for strand in range(2):
+                    for frame in range(3):
+                        n = struct.unpack_from("<Q", data, pos)[0]
+                        per[(side, strand, frame)] = data[pos + 8: pos + 8 + n]
+                        pos += 8 + n
+            out.append(per)
+        return out
     if mode == MODE_TABLES:
         mats = np.frombuffer(data[: 8 * 8 * 1024], dtype=np.int64).reshape(8, 1024).copy()
         maps = np.frombuffer(data[8 * 8 * 1024:], dtype=np.int8).reshape(2, 256).copy()

@@ -19,6 +19,12 @@
  *        1 = 64-bit search (search_64_chunk, heap replay),
  *        2 = 16-bit AVX2 search (search_16_chunk), 3 = 16-bit SSE2 search
  *        4 = dump built-in matrices and maps
+ *        5 = translate every DB sequence (mapped NT codes) with the query
+ *            table (genetic code k) and the DB table (genetic code chunk):
+ *            for side 0/1, strand 0/1, frame 0..2: u64 len, u8 codes[len]
+ *        6 = COMPUTE_ALIGNMENT traceback (align.c align_sequences) of the
+ *            query against every DB sequence: u64 region[4] (q begin, q end,
+ *            d begin, d end), u64 cigar length, cigar bytes
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -40,6 +46,7 @@
 #include "algo/gap_costs.h"
 #include "algo/16/search_16.h"
 #include "algo/64/search_64.h"
+#include "algo/align.h"
 
 int64_t full_sw(sequence_t* dseq, sequence_t* qseq, int64_t* hearray);
 int64_t full_nw(sequence_t* dseq, sequence_t* qseq, int64_t* hearray);
@@ -211,6 +218,43 @@ static void dump_tables(FILE* out) {
     fwrite(map_ncbi_nt16, 1, 256, out);
 }
 
+static void run_translate(FILE* out) {
+    us_init_translation((int)R.k, (int)R.chunk);
+    sequence_t prot = {(char*)malloc(1), 0};
+    for (uint64_t i = 0; i < R.nseq; i++) {
+        sequence_t dna = {(char*)(R.db + R.off[i]), R.off[i + 1] - R.off[i]};
+        for (int side = 0; side < 2; side++)
+            for (int strand = 0; strand < 2; strand++)
+                for (int frame = 0; frame < 3; frame++) {
+                    us_translate_sequence(side, dna, strand, frame, &prot);
+                    uint64_t n = prot.len;
+                    fwrite(&n, 8, 1, out);
+                    fwrite(prot.seq, 1, n, out);
+                }
+    }
+    free(prot.seq);
+}
+
+static void run_align(FILE* out) {
+    score_matrix_64 = (int64_t*)aligned_alloc(64, sizeof(int64_t) * 1024);
+    for (int i = 0; i < 1024; i++) score_matrix_64[i] = R.mat[i];
+    gapO = (int8_t)R.gO;
+    gapE = (int8_t)R.gE;
+    for (uint64_t i = 0; i < R.nseq; i++) {
+        alignment_t al;
+        memset(&al, 0, sizeof al);
+        al.query.seq = (char*)R.q;
+        al.query.len = R.qlen;
+        al.db_seq.seq = (char*)(R.db + R.off[i]);
+        al.db_seq.len = R.off[i + 1] - R.off[i];
+        align_sequences(R.algo == 0 ? SMITH_WATERMAN : NEEDLEMAN_WUNSCH, &al);
+        uint64_t v[5] = {al.align_q_start, al.align_q_end, al.align_d_start, al.align_d_end, al.alignment_len};
+        fwrite(v, 8, 5, out);
+        fwrite(al.alignment, 1, al.alignment_len, out);
+        free(al.alignment);
+    }
+}
+
 int main(int argc, char** argv) {
     if (argc < 3) die("usage: ref_harness <request|-> <response>");
     FILE* f = strcmp(argv[1], "-") ? fopen(argv[1], "rb") : stdin;
@@ -240,6 +284,8 @@ int main(int argc, char** argv) {
     if (!out) die("cannot open response");
     if (R.mode == 0) run_scores(out);
     else if (R.mode == 4) dump_tables(out);
+    else if (R.mode == 5) run_translate(out);
+    else if (R.mode == 6) run_align(out);
     else run_search(out);
     fclose(out);
     return 0;

@@ -344,3 +344,136 @@ def test_nucleotide_both_strands_and_multi_query():
         assert got == exp
     S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
     S.set_chunk_size(1000)
+
+
+def _insertion_order(entries, views_scores, chunk):
+    """Reference 64-bit insertion order (search_64.c:44-56): DB IDs in chunks
+    of `chunk`; within a chunk every query view (outer) over the chunk's
+    entries in adapter order (inner)."""
+    order = []
+    e0 = 0
+    while e0 < len(entries):
+        cend = (entries[e0][0] // chunk + 1) * chunk
+        e1 = e0
+        while e1 < len(entries) and entries[e1][0] < cend:
+            e1 += 1
+        for v, sc in enumerate(views_scores):
+            for e in range(e0, e1):
+                order.append((int(sc[e]), entries[e][0], v, entries[e][1], entries[e][2]))
+        e0 = e1
+    return order
+
+
+@pytest.mark.parametrize("mode", ["TRANS_DB", "TRANS_QUERY", "TRANS_BOTH"])
+@pytest.mark.parametrize("strands", [S.FORWARD_STRAND, S.BOTH_STRANDS, S.COMPLEMENTARY_STRAND])
+def test_translated_search_vs_oracle(mode, strands):
+    """Translated searches: query views x DB entries (strand/frame) in the
+    reference's insertion order; frames translated by the reference-pinned
+    translation (tests/test_translate.py), scores by the oracle."""
+    rng = np.random.default_rng(strands * 7 + len(mode))
+    t = getattr(S, mode)
+    chunk = 23
+    comp = np.array([0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15], np.uint8)
+    # DNA records (lengths >= 2: the reference's (len - frame) / 3 underflows
+    # for shorter ones), a few empty records, IUPAC codes now and then
+    nrec = 160
+    lens = rng.integers(2, 400, nrec)
+    lens[[5, 77]] = 0
+    dna = []
+    for n in lens:
+        c = rng.choice(np.array([1, 2, 4, 8], np.uint8), n)
+        dna.append(np.where(rng.random(n) < 0.05, rng.integers(1, 16, n), c).astype(np.uint8))
+    nt_text = b"-ACMGRSVTWYHKDBN"
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    S.set_output_mode(S.OUTPUT_ERROR)
+    S.init_symbol_translation(t, strands, 1, 1)
+    sel = [s for s in range(2) if (s + 1) & strands]
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "db.fas")
+        if t == S.TRANS_QUERY:
+            prot = [rng.choice(syn.AA_CODES, int(n) // 3).astype(np.uint8) for n in lens]
+            qdna = dna[3][:240] if len(dna[3]) >= 240 else rng.choice(np.array([1, 2, 4, 8], np.uint8), 240)
+            # plant translated query frames in the DB
+            for i, (s, f) in enumerate([(0, 0), (1, 2), (0, 1)]):
+                prot[20 + 40 * i] = np.frombuffer(S.translate(0, qdna.tobytes(), s, f), np.uint8).copy()
+            syn.write_fasta(path, np.concatenate(prot), np.concatenate([[0], np.cumsum([len(p) for p in prot])]).astype(np.uint64))
+            entries = [(i, 0, p) for i, p in enumerate(prot) if len(p)]
+            qviews = [np.frombuffer(S.translate(0, qdna.tobytes(), s, f), np.uint8) for s in sel for f in range(3)]
+            qtext = bytes(nt_text[c] for c in qdna).decode()
+        else:
+            with open(path, "wb") as f:
+                for d in dna:
+                    f.write(b">r\n" + bytes(nt_text[c] for c in d) + b"\n")
+            entries = []
+            for i, d in enumerate(dna):
+                if len(d) == 0:
+                    continue
+                for s in sel:
+                    for fr in range(3):
+                        e = np.frombuffer(S.translate(1, d.tobytes(), s, fr), np.uint8)
+                        entries.append((i, s if strands == S.BOTH_STRANDS else strands, fr, e))
+            entries = [(e[0], e[1], e[2], e[3]) for e in entries]
+            if t == S.TRANS_DB:
+                qprot = np.frombuffer(S.translate(1, dna[9].tobytes(), 0, 1), np.uint8)[:90]
+                qviews = [qprot]
+                qtext = syn.query_string(qprot)
+            else:
+                qdna = dna[9][:300]
+                qviews = [np.frombuffer(S.translate(0, qdna.tobytes(), s, f), np.uint8) for s in sel for f in range(3)]
+                qtext = bytes(nt_text[c] for c in qdna).decode()
+        if t == S.TRANS_QUERY:
+            ent = [(e[0], 0, 0) for e in entries]
+            seqs = [e[2] for e in entries]
+        else:
+            ent = [(e[0], e[1], e[2]) for e in entries]
+            seqs = [e[3] for e in entries]
+        db, off = po.pack_db(seqs)
+        S.init_db(path)
+        S.set_chunk_size(chunk)
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, qtext)
+        assert len(S.query_views(qq)) == len(qviews)
+        for algo in (S.SW, S.NW):
+            vs = [po.scores(algo, qv, db, off, M, -11, -1) for qv in qviews]
+            order = _insertion_order(ent, vs, chunk)
+            for k in (1, 17, 200):
+                exp = po.topk(np.array([o[0] for o in order], np.int64),
+                              np.array([o[1] for o in order], np.uint64), k)
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                got = [(h["score"], h["id"]) for h in fn(qq, k, 16)]
+                assert got == exp, (mode, strands, algo, k, got[:5], exp[:5])
+        S.free_sequence(qq)
+        S.set_chunk_size(1000)
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+
+
+# reference tests/test_libssa.c:48-93 (COMPUTE_ALIGNMENT, 64-bit, 1 thread)
+ALIGN_KAT = {
+    "sw": [(877, 91, "2MD2MIM2I3MD3MD4M2D8M5I3M5IM3I7MI7M3I5MI3M"),
+           (847, 91, "2MD2MIM2I3MD3MD4M2D8M5I3M5IM3I7MI7M3I4MI4M"),
+           (753, 91, "2MD2MIM2I3MD3MD3M2D9M5I3M5IM3I7MI7M3I5MI3M"),
+           (565, 91, "2MD2MIM2I3MD3MD4M2D8M5I3M5IM3I7MI7M3I5MI3M"),
+           (398, 91, "2MD2MIM2I3MD3MD3M2D9M5I3M5IM3I7MI7M3I5MI3M")],
+    "nw": [(1050, 33, "2MI2MI6M3I6MD3M19I4M3IMI3M5I3M5IM3I7MI7M4IMIMI4MI2M7I"),
+           (908, 28, "2MI2MI6M3I6MD3M5IM2I2M3I2M5IMI9MD2M3I3M9I2M3I2M4I2M2IMI4MI2M7I"),
+           (938, 24, "2MI2MI6M3I6MD3M5IM2I2M3I2M5IMI9MD2M3I3M9I2M3I2M4IM3IMIMIM2I5M10I"),
+           (378, 21, "2MI2MI6M3I5M9I2M7IM6IMI3M3I6M5I3M5IM3I7MI7M4IMIMI4MI2M7I"),
+           (75, 12, "2MI2MI6M3I5M9I2M7IM6IMI3M3I6M5I3M5IM3I7MI7M4IMIMI4MI2M7I")],
+}
+
+
+@pytest.mark.parametrize("width", [S.BIT_WIDTH_64, S.BIT_WIDTH_16, S.BIT_WIDTH_8])
+def test_compute_alignment_kat(width):
+    S.set_output_mode(S.OUTPUT_ERROR)
+    S.init_constant_scores(5, -4)
+    S.init_gap_penalties(-4, -2)
+    S.init_symbol_translation(S.NUCLEOTIDE, S.FORWARD_STRAND, 3, 3)
+    S.set_thread_count(1)
+    S.init_db(os.path.join(DATA, "AF091148.fas"))
+    q = S.init_sequence_fasta(S.READ_FROM_FILE, os.path.join(DATA, "one_seq.fas"))
+    for name, fn in (("sw", S.sw_align), ("nw", S.nw_align)):
+        got = [(h["id"], h["score"], h["alignment"]) for h in fn(q, 5, width, S.COMPUTE_ALIGNMENT)]
+        assert got == ALIGN_KAT[name], (name, got)
+    # COMPUTE_SCORE leaves the alignment fields empty
+    assert all(h["alignment"] is None for h in S.sw_align(q, 5, width, S.COMPUTE_SCORE))
+    S.free_sequence(q)
+    S.set_thread_count(0)

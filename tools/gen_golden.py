@@ -11,6 +11,14 @@ outputs as data:
   tests/golden/kat.json        known-answer cases of the reference's own tests
                                 with the full top-k the reference's
                                64-bit and AVX2 16-bit searches return
+  tests/golden/translate.npz   random nucleotide sequences (IUPAC codes
+                               included) translated by the reference's
+                               us_translate_sequence for every valid genetic
+                               code, both sides, strands and frames
+  tests/golden/align.json      COMPUTE_ALIGNMENT regions + CIGARs of the
+                               reference's align_sequences (align.c, cigar.c)
+                               on seeded pairs: SW and NW, NT constant scoring,
+                               BLOSUM62, an asymmetric matrix
   tests/golden/random_*.npz    seeded synthetic DBs (regenerated from their
                                parameters by libssa_amd.synthetic) with the
                                reference's full int64 score vector (full_sw /
@@ -121,5 +129,97 @@ def main():
         print(tag, "ok", out["sw_top10"][:3])
 
 
+VALID_GENCODES = [1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 21, 22, 23]
+
+
+def gen_translate():
+    """Reference translations (util_sequence.c:332-382) of seeded random NT
+    code sequences: query table = code g, DB table = the next valid code."""
+    rng = np.random.default_rng(2024)
+    arrays = {}
+    for gi, g in enumerate(VALID_GENCODES):
+        d = VALID_GENCODES[(gi + 1) % len(VALID_GENCODES)]
+        lens = [2, 3, 4, 5, 6, 7, 8, 9] + list(rng.integers(10, 90, 24))
+        seqs = []
+        for n in lens:
+            # mostly concrete bases (A C G T = 1 2 4 8), some IUPAC ambiguity codes
+            conc = rng.choice(np.array([1, 2, 4, 8], np.uint8), n)
+            amb = rng.integers(1, 16, n).astype(np.uint8)
+            seqs.append(np.where(rng.random(n) < 0.15, amb, conc).astype(np.uint8))
+        res = po.ref_run(po.MODE_TRANSLATE, k=g, chunk=d, seqs=seqs)
+        db, off = po.pack_db(seqs)
+        outs, ooff = [], [0]
+        for per in res:
+            for side in range(2):
+                for strand in range(2):
+                    for frame in range(3):
+                        b = np.frombuffer(per[(side, strand, frame)], np.uint8)
+                        outs.append(b)
+                        ooff.append(ooff[-1] + len(b))
+        arrays[f"g{g}_d{d}_db"] = db
+        arrays[f"g{g}_d{d}_off"] = off
+        arrays[f"g{g}_d{d}_out"] = np.concatenate(outs) if outs else np.zeros(0, np.uint8)
+        arrays[f"g{g}_d{d}_outoff"] = np.array(ooff, np.uint64)
+    np.savez_compressed(os.path.join(G, "translate.npz"), **arrays)
+    print("translate ok", len(arrays) // 4, "code pairs")
+
+
+def _mutate(rng, seq, alphabet, ident):
+    out = []
+    for c in seq:
+        r = rng.random()
+        if r < (1 - ident) * 0.7:
+            out.append(rng.choice(alphabet))
+        elif r < (1 - ident) * 0.85:
+            continue
+        elif r < (1 - ident):
+            out += [c, rng.choice(alphabet)]
+        else:
+            out.append(c)
+    return np.array(out if out else [alphabet[0]], np.uint8)
+
+
+def gen_align():
+    """Reference traceback (align_sequences) on seeded (query, DB) pairs."""
+    rng = np.random.default_rng(77)
+    mats = po.ref_run(po.MODE_TABLES)[0]
+    nt = np.array([1, 2, 4, 8], np.uint8)
+    asym = np.full(1024, -1, np.int64)
+    for x in syn.AA_CODES:
+        for y in syn.AA_CODES:
+            asym[(int(x) << 5) + int(y)] = int(rng.integers(-6, 9))
+    cases = [("nt_const5_4", nt, po.matrix_constant(5, -4), -4, -2),
+             ("aa_blosum62", syn.AA_CODES, mats[NAMES.index("blosum62")], -11, -1),
+             ("aa_asym", syn.AA_CODES, asym, -5, -2)]
+    out = []
+    for name, alpha, M, go, ge in cases:
+        for t in range(4):
+            q = rng.choice(alpha, int(rng.integers(5, 120))).astype(np.uint8)
+            seqs = []
+            for i in range(40):
+                if i % 3 == 0:
+                    seqs.append(_mutate(rng, q, alpha, rng.uniform(0.5, 0.95)))
+                else:
+                    seqs.append(rng.choice(alpha, int(rng.integers(1, 150))).astype(np.uint8))
+            sw = po.scores(0, q, *po.pack_db(seqs), M, go, ge)
+            keep = [s for s, v in zip(seqs, sw) if v > 0]   # score-0 SW regions are UB in the reference
+            for algo in (0, 1):
+                res = po.ref_run(po.MODE_ALIGN, algo, q, keep, M, go, ge)
+                for s, (reg, cig) in zip(keep, res):
+                    out.append({"case": name, "algo": algo, "gap_open": go, "gap_extend": ge,
+                                "matrix": name, "query": q.tolist(), "db": s.tolist(),
+                                "region": list(reg), "cigar": cig})
+    mats_used = {name: [int(x) for x in M] for name, _, M, _, _ in cases}
+    json.dump({"matrices": mats_used, "pairs": out}, open(os.path.join(G, "align.json"), "w"))
+    print("align ok", len(out), "pairs")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "translate":
+        gen_translate()
+    elif len(sys.argv) > 1 and sys.argv[1] == "align":
+        gen_align()
+    else:
+        main()
+        gen_translate()
+        gen_align()
