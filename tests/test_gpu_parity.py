@@ -387,6 +387,8 @@ def test_translated_search_vs_oracle(mode, strands):
     M = TABLES["matrices"][NAMES.index("blosum62")].copy()
     S.set_output_mode(S.OUTPUT_ERROR)
     S.init_symbol_translation(t, strands, 1, 1)
+    S.init_score_matrix(S.MATRIX_BUILDIN, "blosum62")
+    S.init_gap_penalties(-11, -1)
     sel = [s for s in range(2) if (s + 1) & strands]
     with tempfile.TemporaryDirectory() as tmp:
         path = os.path.join(tmp, "db.fas")
