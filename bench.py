@@ -12,7 +12,14 @@ N>1 each rank searches its own 1 M-sequence shard of an N M-sequence DB
 log, the logs are gathered to rank 0 over RCCL and replayed there
 (ssa_amd_replay), giving the bit-exact global result.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--seqs S] [--algo sw|nw]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--seqs S]
+
+Other BASELINE.json configurations (parity/extra measurements; the default
+line is C2): --config c3 = NW BLOSUM50 -10/-2, 1000-residue query, 1 M
+sequences per GPU; c4 = SW BLOSUM62 -11/-1 (API width 8) over 10 M sequences
+split across the ranks (strong scaling); c5 = SW DNA +5/-4, gaps -4/-2,
+10 k-nt query vs 50 M reads of 150 nt split across the ranks (strong).
+--seqs overrides the per-GPU sequence count of any config.
 """
 import argparse
 import json
@@ -41,18 +48,49 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--seqs", type=int, default=1_000_000, help="DB sequences per GPU")
-    p.add_argument("--qlen", type=int, default=400)
-    p.add_argument("--algo", default="sw", choices=["sw", "nw"])
-    p.add_argument("--matrix", default="blosum62")
-    p.add_argument("--gap-open", type=int, default=-11)
-    p.add_argument("--gap-extend", type=int, default=-1)
+    p.add_argument("--config", default="c2", choices=list(CONFIGS))
+    p.add_argument("--seqs", type=int, default=None, help="DB sequences per GPU (default: the config's)")
+    p.add_argument("--qlen", type=int, default=None)
+    p.add_argument("--algo", default=None, choices=["sw", "nw"])
+    p.add_argument("--matrix", default=None)
+    p.add_argument("--gap-open", type=int, default=None)
+    p.add_argument("--gap-extend", type=int, default=None)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--strip-np", type=int, default=16)
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
-    return p.parse_args()
+    args = p.parse_args()
+    cfg = CONFIGS[args.config]
+    for key in ("qlen", "algo", "matrix", "gap_open", "gap_extend"):
+        if getattr(args, key) is None:
+            setattr(args, key, cfg[key])
+    args.db = cfg["db"]
+    args.width = cfg["width"]
+    args.strong = cfg["total_seqs"] is not None
+    return args
+
+
+# BASELINE.json configs; "total_seqs" set = strong scaling (split across ranks)
+CONFIGS = {
+    "c2": dict(algo="sw", matrix="blosum62", gap_open=-11, gap_extend=-1, qlen=400, db="protein",
+               seqs=1_000_000, total_seqs=None, width=16),
+    "c3": dict(algo="nw", matrix="blosum50", gap_open=-10, gap_extend=-2, qlen=1000, db="protein",
+               seqs=1_000_000, total_seqs=None, width=16),
+    "c4": dict(algo="sw", matrix="blosum62", gap_open=-11, gap_extend=-1, qlen=400, db="protein",
+               seqs=None, total_seqs=10_000_000, width=8),
+    "c5": dict(algo="sw", matrix="const5_-4", gap_open=-4, gap_extend=-2, qlen=10_000, db="dna",
+               seqs=None, total_seqs=50_000_000, width=16),
+}
+
+
+def matrix_table(name):
+    from oracle import pyoracle as po
+    if name.startswith("const"):
+        a, b = name[5:].split("_")
+        return po.matrix_constant(int(a), int(b))
+    tabs = np.load(os.path.join(ROOT, "tests", "golden", "tables.npz"))
+    return tabs["matrices"][[str(x) for x in tabs["names"]].index(name)].copy()
 
 
 def cpu_baseline(codes, off, q, M, args, cores):
@@ -112,31 +150,47 @@ def main():
     for o in args.option:
         k, v = o.split("=")
         S.set_option(k, int(v))
-    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
-    S.init_score_matrix(S.MATRIX_BUILDIN, args.matrix)
+    dna = args.db == "dna"
+    S.init_symbol_translation(S.NUCLEOTIDE if dna else S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+    if args.matrix.startswith("const"):
+        a, b = args.matrix[5:].split("_")
+        S.init_constant_scores(int(a), int(b))
+    else:
+        S.init_score_matrix(S.MATRIX_BUILDIN, args.matrix)
     S.init_gap_penalties(args.gap_open, args.gap_extend)
     algo = S.SW if args.algo == "sw" else S.NW
+    cfg = CONFIGS[args.config]
+    if args.seqs is None:
+        args.seqs = cfg["seqs"] if cfg["total_seqs"] is None else (cfg["total_seqs"] + world - 1) // world
 
     # --- synthetic shard (untimed): generate, write FASTA, pack into HBM
     t0 = time.time()
-    q = syn.protein_query(args.qlen, 7)
-    codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000)
+    if dna:
+        q = syn.dna_query(args.qlen, 8)
+        codes, off = syn.dna_reads(args.seqs, 150, 43 + 1000 * rank, query=q, plant_every=100000)
+    else:
+        q = syn.protein_query(args.qlen, 7)
+        codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000, sampler="lut")
     tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
     path = os.path.join(tmpdir, "db.fas")
-    syn.write_fasta(path, codes, off)
+    syn.write_fasta(path, codes, off, nucleotide=dna)
+    gen_s = time.time() - t0
+    t1 = time.time()
     S.init_db(path)
     S.set_id_offset(rank * args.seqs)
     S.prepare_db()
-    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    os.remove(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
+    load_s = time.time() - t1
     setup_s = time.time() - t0
     cells_local = float(off[-1]) * args.qlen
 
     def step():
         if world == 1:
             fn = S.sw_align if algo == S.SW else S.nw_align
-            return [(h["score"], h["id"]) for h in fn(qq, args.k, S.BIT_WIDTH_16)]
+            return [(h["score"], h["id"]) for h in fn(qq, args.k, args.width)]
         from libssa_amd.dist import global_topk
-        log = S.search(qq, algo, args.k, S.BIT_WIDTH_16, S.LOG)
+        log = S.search(qq, algo, args.k, args.width, S.LOG)
         return global_topk(log, args.k, dist, rank, world, dev)
 
     def sync():
@@ -148,13 +202,17 @@ def main():
     for _ in range(args.warmup):
         step()
     sync()
-    kernel_ms, wide_ms = [], []
+    kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms = [], [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
         st = S.stats()
         kernel_ms.append(st["kernel_ms"])
         wide_ms.append(st["wide_ms"])
+        search_ms.append(st["search_ms"])
+        prep_ms.append(st["prep_ms"])
+        d2h_ms.append(st["d2h_ms"])
+        replay_ms.append(st["replay_ms"])
     sync()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
@@ -196,15 +254,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "i16",
         "data": "synthetic",
-        "config": {"workload": f"{args.algo.upper()} int16 {args.matrix} gaps {args.gap_open}/{args.gap_extend}, "
-                               f"{args.qlen}-aa query vs {args.seqs} synthetic protein seqs per GPU "
+        "config": {"workload": f"{args.config.upper()}: {args.algo.upper()} {args.matrix} gaps {args.gap_open}/{args.gap_extend}, "
+                               f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
                                f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
                    "db_seqs_per_gpu": args.seqs, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
-                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "strip_np": args.strip_np},
+                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "strip_np": args.strip_np,
+                   "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
@@ -213,13 +272,16 @@ def main():
                    "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,
                    "valu_issue_frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None,
                    "valu_instr_per_cell": instr_per_cell},
+        "host_ms": {"search_call": round(float(np.mean(search_ms)), 3), "prep": round(float(np.mean(prep_ms)), 3), "d2h_filter": round(float(np.mean(d2h_ms)), 3),
+                    "replay": round(float(np.mean(replay_ms)), 3)},
         "setup_s": round(setup_s, 1),
+        "setup": {"generate_and_write_fasta_s": round(gen_s, 1), "init_db_and_pack_s": round(load_s, 1),
+                  "pack_ms": round(st["pack_ms"], 1)},
         "top_hit": list(res[0]) if res else None,
     }
     if world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle as po
-        tabs = np.load(os.path.join(ROOT, "tests", "golden", "tables.npz"))
-        M = tabs["matrices"][[str(x) for x in tabs["names"]].index(args.matrix)].copy()
+        M = matrix_table(args.matrix)
         cores = min(16, os.cpu_count() or 1)
         try:
             out["cpu_baseline"] = cpu_baseline(codes, off, q, M, args, cores)

@@ -52,6 +52,7 @@ typedef struct {
     int32_t device;
     uint64_t kernel_bytes;   /* algorithmic HBM bytes of the strip kernels */
     char kernel[32];         /* main scoring kernel of the last search, e.g. "pair_f16_sw" */
+    double prep_ms;          /* host work before the first kernel launch (profiles, uploads) */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0

@@ -47,6 +47,10 @@ void replay(const SearchScores& sc, const EntryMeta& meta, const std::vector<Que
         if (heap.add(h) && log) log->push_back(h);
     };
     (void)views;
+    if (sc.sparse) {
+        for (const uint32_t e : sc.cand) visit(0, e);
+        return;
+    }
     if (V == 1) {
         if (sc.wide.empty()) {
             // hot loop: plain int32 scan with the root cached
@@ -75,6 +79,22 @@ void replay(const SearchScores& sc, const EntryMeta& meta, const std::vector<Que
 void overflow_counters(const SearchScores& sc, int algo, int bw, uint64_t& o8, uint64_t& o16) {
     o8 = o16 = 0;
     if (bw == BIT_WIDTH_64) return;
+    if (sc.sparse) {
+        // device counts over the int32 scores + the exactly re-scored entries
+        o8 = bw == BIT_WIDTH_8 ? sc.dev_o8 : 0;
+        o16 = sc.dev_o16;
+        for (const auto& w : sc.wide) {
+            const int64_t s = w.second;
+            if (algo == kAlgoSW) {
+                if (bw == BIT_WIDTH_8 && s >= 255) o8++;
+                if (s >= 65535) o16++;
+            } else {
+                if (bw == BIT_WIDTH_8 && (s <= -128 || s >= 127)) o8++;
+                if (s <= -32768 || s >= 32767) o16++;
+            }
+        }
+        return;
+    }
     for (size_t v = 0; v < sc.views; v++)
         for (size_t e = 0; e < sc.entries; e++) {
             const int64_t s = sc.get(v, e);
@@ -99,7 +119,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     ensure_device_db();
     R.views = query_views(q);
     SearchScores sc;
-    device_search(R.views, algo, sc);
+    device_search(R.views, algo, k, bw, sc);
     const double t1 = now_ms();
     TopK heap(k);
     replay(sc, device_db().meta, R.views, heap, want_log ? &R.hits : nullptr);
@@ -315,6 +335,7 @@ void ssa_amd_set_option(const char* name, long value) {
     if (!strcmp(name, "strip_np")) cfg().strip_np = (int)value;
     else if (!strcmp(name, "force_wide")) cfg().force_wide = (int)value;
     else if (!strcmp(name, "sw_kernel")) cfg().sw_kernel = (int)value;
+    else if (!strcmp(name, "no_filter")) cfg().no_filter = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -33,6 +33,7 @@ struct Config {
     int waves_per_block = 4;
     int force_wide = 0;                   // 1: score everything with the int64 kernel
     int sw_kernel = 0;                    // 0: f16-pattern kernel when applicable, 1: int16 kernel
+    int no_filter = 0;                    // 1: copy every score back (no device top-k filter)
 };
 Config& cfg();
 

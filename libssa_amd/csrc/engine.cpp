@@ -43,6 +43,12 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
     dfree(d_work); dfree(d_smax);
+    dfree(d_cand); dfree(d_cand_score); dfree(d_summary); dfree(d_thresh); dfree(d_fcount);
+    if (h_cand) (void)hipHostFree(h_cand);
+    if (h_cand_score) (void)hipHostFree(h_cand_score);
+    if (h_fcount) (void)hipHostFree(h_fcount);
+    d_cand = nullptr; d_cand_score = nullptr; d_summary = nullptr; d_thresh = nullptr; d_fcount = nullptr;
+    h_cand = nullptr; h_cand_score = nullptr; h_fcount = nullptr; h_cand_cap = 0;
     if (h_scores) (void)hipHostFree(h_scores);
     if (h_ovf) (void)hipHostFree(h_ovf);
     if (h_wide) (void)hipHostFree(h_wide);
@@ -246,6 +252,18 @@ void ensure_device_db() {
     dalloc((void**)&D.d_lane_len, lane_len.size() * 4, "lane_len");
     dalloc((void**)&D.d_lane_out, lane_out.size() * 4, "lane_out");
     dalloc((void**)&D.d_smax, lane_out.size() * 4, "running max");
+    {
+        const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
+        dalloc((void**)&D.d_cand, std::max<size_t>(E, 1) * 4, "candidates");
+        dalloc((void**)&D.d_cand_score, std::max<size_t>(E, 1) * 4, "candidate scores");
+        dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
+        dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
+        dalloc((void**)&D.d_fcount, 16, "filter counters");
+        D.h_cand_cap = 1 << 16;
+        check(hipHostMalloc((void**)&D.h_cand, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
+        check(hipHostMalloc((void**)&D.h_cand_score, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
+        check(hipHostMalloc((void**)&D.h_fcount, 16, hipHostMallocDefault), "pinned");
+    }
     dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
     dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
     dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
@@ -258,6 +276,8 @@ void ensure_device_db() {
     check(hipMemcpy(D.d_lane_out, lane_out.data(), lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
     D.ngroups = ngroups;
     D.nblocks = blocks;
+    D.len_sorted = S.meta.len;
+    std::sort(D.len_sorted.begin(), D.len_sorted.end());
     D.meta = std::move(S.meta);
     D.lane_out = std::move(lane_out);
     D.code_of = std::move(code_of);
@@ -319,7 +339,7 @@ static uint32_t nw_f16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM,
     return (uint32_t)a;
 }
 
-void device_search(const std::vector<QueryView>& views, int algo, SearchScores& out) {
+void device_search(const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out) {
     DeviceDB& D = device_db();
     check(hipSetDevice(D.device), "hipSetDevice");
     const Config& C = cfg();
@@ -340,6 +360,12 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
     out.views = V;
     out.wide.clear();
     out.cells = 0;
+    out.cand.clear();
+    out.dev_o8 = out.dev_o16 = 0;
+    // single query view and a small k: only heap-changing candidates come back
+    const double t_prep0 = now_ms();
+    double prep = 0;
+    out.sparse = V == 1 && k > 0 && k <= (size_t)kFilterMaxK && E > 0 && views[0].len > 0 && !cfg().no_filter;
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
     uint64_t kernel_bytes = 0;
@@ -381,8 +407,8 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         if (nw && C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
             nmax_f16 = std::min(nw_f16_limit(m, Q, R, minM, maxM, &nw_base), nmax16);
             if (nmax_f16 > 0) {
-                size_t beyond = 0;
-                for (size_t e = 0; e < E; e++) beyond += D.meta.len[e] > nmax_f16;
+                const size_t beyond = (size_t)(D.len_sorted.end() -
+                                               std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), nmax_f16));
                 use_nwf16 = beyond <= 64;
             }
         }
@@ -396,11 +422,18 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
         const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
-        auto val = [&](uint32_t c, size_t i) -> int16_t {
-            if (c >= A || i >= m) return padv;
-            const int64_t x = M[(D.code_of[c] << 5) + qv.seq[i]];
-            return (int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, x));
-        };
+        // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
+        // rows up to the last strip's end so table builders need no bounds test
+        const size_t mpad = (size_t)nstrips * 2 * np + 64;
+        std::vector<uint16_t> P((size_t)(A + 1) * mpad, (uint16_t)padv);
+        for (uint32_t c = 0; c < A; c++) {
+            const int64_t* row = M + ((size_t)D.code_of[c] << 5);
+            uint16_t* pc = P.data() + (size_t)c * mpad;
+            for (size_t i = 0; i < m; i++)
+                pc[i] = (uint16_t)(int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, row[qv.seq[i]]));
+        }
+        auto prow_of = [&](uint32_t c) { return P.data() + (size_t)std::min(c, A) * mpad; };
+        auto val = [&](uint32_t c, size_t i) -> int16_t { return (int16_t)prow_of(c)[i]; };
         struct PairLaunch { int np; uint32_t row0, nstrips; size_t qoff; uint32_t flags; bool cap; };
         std::vector<PairLaunch> plan;
         std::vector<uint32_t> qpt;
@@ -410,17 +443,20 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
             const uint32_t full = (uint32_t)(m / 32), rem = (uint32_t)(m % 32);
             const bool tail = rem > 0 && rem <= 16;
             const uint32_t nmain = tail || rem == 0 ? full : full + 1;
-            auto add_tables = [&](int P, uint32_t row0, uint32_t count) {
+            auto add_tables = [&](int Ph, uint32_t row0, uint32_t count) {
                 const size_t off = qpt.size();
-                qpt.resize(off + (size_t)count * prow * prow * P);
-                for (uint32_t s = 0; s < count; s++)
-                    for (uint32_t c1 = 0; c1 < prow; c1++)
-                        for (uint32_t c0 = 0; c0 < prow; c0++)
-                            for (int r = 0; r < P; r++) {
-                                const size_t i = row0 + (size_t)s * 2 * P + r;
-                                qpt[off + (((size_t)s * prow + c1) * prow + c0) * P + r] =
-                                    (uint32_t)(uint16_t)val(c1, i) | ((uint32_t)(uint16_t)val(c0, i + P) << 16);
-                            }
+                qpt.resize(off + (size_t)count * prow * prow * Ph);
+                uint32_t* dst = qpt.data() + off;
+                for (uint32_t s = 0; s < count; s++) {
+                    const size_t i0 = row0 + (size_t)s * 2 * Ph;
+                    for (uint32_t c1 = 0; c1 < prow; c1++) {
+                        const uint16_t* lo = prow_of(c1) + i0;
+                        for (uint32_t c0 = 0; c0 < prow; c0++) {
+                            const uint16_t* hi = prow_of(c0) + i0 + Ph;
+                            for (int r = 0; r < Ph; r++) *dst++ = (uint32_t)lo[r] | ((uint32_t)hi[r] << 16);
+                        }
+                    }
+                }
                 return off;
             };
             const uint32_t nbulk = nw && !tail ? nmain - 1 : nmain;
@@ -508,6 +544,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
+        if (v == 0) prep = now_ms() - t_prep0;
         check(hipEventRecord(D.ev[0], st), "event");
         if (use_pair) {
             for (const PairLaunch& l : plan) {
@@ -524,11 +561,51 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
         check(hipEventRecord(D.ev[1], st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         check(hipEventRecord(D.ev[2], st), "event");
-        check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
+        if (out.sparse) {
+            FilterArgs f{};
+            f.scores = D.d_scores;
+            f.n = (uint32_t)E;
+            f.k = (uint32_t)k;
+            f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
+            f.nw = nw ? 1 : 0;
+            f.bw = bw;
+            f.summary = D.d_summary;
+            f.thresh = D.d_thresh;
+            f.cand = D.d_cand;
+            f.cand_score = D.d_cand_score;
+            f.counters = D.d_fcount;
+            check(hipMemsetAsync(D.d_fcount, 0, 16, st), "memset");
+            check(launch_filter(f, st), "filter launch");
+            check(hipMemcpyAsync(D.h_fcount, D.d_fcount, 16, hipMemcpyDeviceToHost, st), "D2H counters");
+            // optimistic copy of the first candidates (usually all of them)
+            const size_t first = std::min(D.h_cand_cap, E);
+            check(hipMemcpyAsync(D.h_cand, D.d_cand, 4 * first, hipMemcpyDeviceToHost, st), "D2H cand");
+            check(hipMemcpyAsync(D.h_cand_score, D.d_cand_score, 4 * first, hipMemcpyDeviceToHost, st),
+                  "D2H cand scores");
+        } else {
+            check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
+        }
         check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
         check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
         check(hipEventRecord(D.ev[3], st), "event");
         check(hipStreamSynchronize(st), "search");
+        if (out.sparse) {
+            const uint32_t nc = D.h_fcount[0];
+            if (nc > D.h_cand_cap) {
+                (void)hipHostFree(D.h_cand);
+                (void)hipHostFree(D.h_cand_score);
+                D.h_cand_cap = std::max<size_t>(nc, 2 * D.h_cand_cap);
+                check(hipHostMalloc((void**)&D.h_cand, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
+                check(hipHostMalloc((void**)&D.h_cand_score, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
+                check(hipMemcpy(D.h_cand, D.d_cand, 4 * (size_t)nc, hipMemcpyDeviceToHost), "D2H cand");
+                check(hipMemcpy(D.h_cand_score, D.d_cand_score, 4 * (size_t)nc, hipMemcpyDeviceToHost), "D2H cand");
+            }
+            out.cand.assign(D.h_cand, D.h_cand + nc);
+            for (uint32_t i = 0; i < nc; i++) hs[D.h_cand[i]] = D.h_cand_score[i];
+            std::sort(out.cand.begin(), out.cand.end());
+            out.dev_o8 += D.h_fcount[1];
+            out.dev_o16 += D.h_fcount[2];
+        }
         uint32_t nov = D.h_ovf[0];
         if (nov > kOvfCap) fatal("overflow list exhausted (%u entries)", nov);
         if (nov > 4096) {
@@ -552,6 +629,7 @@ void device_search(const std::vector<QueryView>& views, int algo, SearchScores& 
     }
     ssa_amd_stats_t& S = stats();
     S.kernel_ms = kms;
+    S.prep_ms = V == 1 ? prep : 0;
     S.wide_ms = wms;
     S.d2h_ms = dms;
     S.cells = out.cells;

@@ -38,6 +38,16 @@ struct DeviceDB {
     uint32_t* d_lane_len = nullptr;
     uint32_t* d_lane_out = nullptr;
     uint32_t* d_smax = nullptr;           // SW running max between pair_kernel launches
+    // top-k candidate filter (kernels.h FilterArgs)
+    uint32_t* d_cand = nullptr;
+    int32_t* d_cand_score = nullptr;
+    int32_t* d_summary = nullptr;
+    int32_t* d_thresh = nullptr;
+    uint32_t* d_fcount = nullptr;
+    uint32_t* h_cand = nullptr;           // pinned, h_cand_cap entries
+    int32_t* h_cand_score = nullptr;
+    uint32_t* h_fcount = nullptr;
+    size_t h_cand_cap = 0;
     int32_t* d_scores = nullptr;
     int32_t* h_scores = nullptr;          // pinned, [views][entries]
     size_t h_scores_cap = 0;
@@ -53,6 +63,7 @@ struct DeviceDB {
     int64_t* d_work = nullptr;
     size_t work_cap = 0;
     std::vector<uint32_t> lane_out;       // host copy for overflow mapping
+    std::vector<uint32_t> len_sorted;     // entry lengths, ascending
     // residues are stored in a compact alphabet: device code c < alpha stands
     // for residue code code_of[c]; code alpha is the padding column
     std::vector<uint8_t> code_of;
@@ -69,6 +80,12 @@ std::vector<uint8_t> fetch_entry_codes(uint64_t local_id, int strand, int frame)
 struct SearchScores {
     const int32_t* s32 = nullptr;
     size_t entries = 0, views = 0;
+    // sparse: only the entries in `cand` (ascending) were copied back -- the
+    // device filter proved every other entry leaves the top-k heap unchanged;
+    // o8/o16 then come from the device counters (non-overflowed entries)
+    bool sparse = false;
+    std::vector<uint32_t> cand;
+    uint64_t dev_o8 = 0, dev_o16 = 0;
     std::unordered_map<uint64_t, int64_t> wide;   // key = view * entries + entry
     uint64_t cells = 0;
     int64_t get(size_t v, size_t e) const {
@@ -78,7 +95,8 @@ struct SearchScores {
         return it == wide.end() ? (int64_t)INT32_MIN : it->second;
     }
 };
-void device_search(const std::vector<QueryView>& views, int algo, SearchScores& out);
+// k / bit_width decide whether the device top-k filter applies
+void device_search(const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out);
 
 ssa_amd_stats_t& stats();
 void check(hipError_t e, const char* what);

@@ -57,6 +57,26 @@ struct WideArgs {
     uint32_t ovf_cap;
 };
 
+// Device-side top-k candidate filter (single query view, k <= kFilterMaxK).
+// Block b of kFilterBlock consecutive entries (insertion order) gets as
+// threshold T[b] the k-th largest of the earlier blocks' maxima -- a lower
+// bound of the reference heap's root whenever one of its entries is
+// offered -- and only entries with score > T[b] (or overflowed, INT32_MIN)
+// can change the heap.  They are compacted into cand[] for the host replay.
+constexpr int kFilterBlock = 4096;
+constexpr int kFilterMaxK = 64;
+struct FilterArgs {
+    const int32_t* scores;     // [n] per-entry scores, INT32_MIN = overflowed (exact value elsewhere)
+    uint32_t n, k, nblocks;
+    int32_t nw, bw;            // counters follow the reference's overflow rules
+    int32_t* summary;          // [nblocks] block maxima
+    int32_t* thresh;           // [nblocks]
+    uint32_t* cand;            // [n] candidate entry indices (unordered)
+    int32_t* cand_score;       // [n] their scores
+    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows
+};
+hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
+
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st);

@@ -479,3 +479,44 @@ def test_compute_alignment_kat(width):
     assert all(h["alignment"] is None for h in S.sw_align(q, 5, width, S.COMPUTE_SCORE))
     S.free_sequence(q)
     S.set_thread_count(0)
+
+
+@pytest.mark.parametrize("pattern", ["ties", "rising", "random"])
+def test_device_topk_filter_matches_full_scan(pattern):
+    """The device candidate filter (kernels.hip filter_*) must give exactly
+    the host full-scan result: heavy ties, scores rising with the ID (most
+    entries are candidates: exercises the > 64 K candidate path), random."""
+    rng = np.random.default_rng(len(pattern))
+    q = syn.protein_query(50, 3)
+    n = 90000
+    if pattern == "ties":
+        seqs = [q[:30].copy() for _ in range(n)]
+    elif pattern == "rising":
+        seqs = [np.concatenate([q[: 1 + (i * 49) // n], rng.choice(syn.AA_CODES, 5)]).astype(np.uint8)
+                for i in range(n)]
+    else:
+        seqs = [rng.choice(syn.AA_CODES, int(rng.integers(5, 80))).astype(np.uint8) for _ in range(n)]
+    codes = np.concatenate(seqs)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+            for k in (1, 2, 10, 64):
+                for width in (8, 16):
+                    S.set_option("no_filter", 1)
+                    full = [(h["score"], h["id"]) for h in fn(qq, k, width)]
+                    st_full = S.stats()
+                    S.set_option("no_filter", 0)
+                    got = [(h["score"], h["id"]) for h in fn(qq, k, width)]
+                    st = S.stats()
+                    assert got == full, (pattern, algo, k)
+                    assert (st["overflow_8"], st["overflow_16"]) == (st_full["overflow_8"], st_full["overflow_16"])
+                    log_full = None
+            S.set_option("no_filter", 1)
+            log_full = S.search(qq, algo, 7, 16, S.LOG)
+            S.set_option("no_filter", 0)
+            assert S.search(qq, algo, 7, 16, S.LOG) == log_full
+        S.free_sequence(qq)
