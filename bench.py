@@ -202,7 +202,7 @@ def main():
     for _ in range(args.warmup):
         step()
     sync()
-    kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms = [], [], [], [], [], []
+    kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms, upload_ms, sync_ms = [], [], [], [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -211,6 +211,8 @@ def main():
         wide_ms.append(st["wide_ms"])
         search_ms.append(st["search_ms"])
         prep_ms.append(st["prep_ms"])
+        upload_ms.append(st["upload_ms"])
+        sync_ms.append(st["sync_wait_ms"])
         d2h_ms.append(st["d2h_ms"])
         replay_ms.append(st["replay_ms"])
     sync()
@@ -272,7 +274,8 @@ def main():
                    "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,
                    "valu_issue_frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None,
                    "valu_instr_per_cell": instr_per_cell},
-        "host_ms": {"search_call": round(float(np.mean(search_ms)), 3), "prep": round(float(np.mean(prep_ms)), 3), "d2h_filter": round(float(np.mean(d2h_ms)), 3),
+        "host_ms": {"search_call": round(float(np.mean(search_ms)), 3), "prep": round(float(np.mean(prep_ms)), 3),
+                    "upload": round(float(np.mean(upload_ms)), 3), "sync_wait": round(float(np.mean(sync_ms)), 3), "d2h_filter": round(float(np.mean(d2h_ms)), 3),
                     "replay": round(float(np.mean(replay_ms)), 3)},
         "setup_s": round(setup_s, 1),
         "setup": {"generate_and_write_fasta_s": round(gen_s, 1), "init_db_and_pack_s": round(load_s, 1),

@@ -53,6 +53,8 @@ typedef struct {
     uint64_t kernel_bytes;   /* algorithmic HBM bytes of the strip kernels */
     char kernel[32];         /* main scoring kernel of the last search, e.g. "pair_f16_sw" */
     double prep_ms;          /* host work before the first kernel launch (profiles, uploads) */
+    double upload_ms;        /* device time of the per-search uploads before the first kernel */
+    double sync_wait_ms;     /* host time blocked in the final stream synchronisation */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -76,6 +78,16 @@ size_t ssa_amd_search( p_query query, int algo, size_t hitcount, int bit_width, 
 /* Replays an insertion log (concatenated shard logs, in shard order) and
  * writes the sorted top-k (score desc, id desc).  Returns the count. */
 size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );
+
+/* Persistent packed DB: ssa_amd_save_db writes the device
+ * layout of the open DB (packing it first if needed); ssa_amd_load_db,
+ * called after init_db on the same DB file and with the same
+ * init_symbol_translation settings, uploads that layout instead of
+ * re-reading, mapping and packing every record.  The file records symbol
+ * type, strands, DB genetic code and record count and is refused when they
+ * differ.  Both return 0 on success. */
+int ssa_amd_save_db( const char * path );
+int ssa_amd_load_db( const char * path );
 
 /* COMPUTE_ALIGNMENT traceback of one (query, DB sequence) pair of mapped
  * codes with the current matrix and gap penalties (reference align.c +

@@ -64,7 +64,8 @@ class ssa_amd_stats_t(Structure):
                 ("replay_ms", c_double), ("pack_ms", c_double), ("cells", c_uint64), ("entries", c_uint64),
                 ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
                 ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64),
-                ("kernel", ctypes.c_char * 32), ("prep_ms", c_double)]
+                ("kernel", ctypes.c_char * 32), ("prep_ms", c_double), ("upload_ms", c_double),
+                ("sync_wait_ms", c_double)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -78,7 +79,8 @@ EXPORTS = {
                       "init_db", "init_sequence_fasta", "free_sequence", "sw_align", "nw_align", "free_alignment",
                       "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
                       "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
-                      "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair"],
+                      "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
+                      "ssa_amd_save_db", "ssa_amd_load_db"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -112,6 +114,7 @@ def load():
         "ssa_amd_search": ([P, c_int, c_size_t, c_int, c_int, POINTER(ssa_hit_t), c_size_t], c_size_t),
         "ssa_amd_replay": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
         "ssa_amd_query_views": ([P, POINTER(q_seq_t), c_size_t], c_size_t),
+        "ssa_amd_save_db": ([c_char_p], c_int), "ssa_amd_load_db": ([c_char_p], c_int),
         "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
                                c_size_t),
         "ssa_amd_translate": ([c_int, c_char_p, c_size_t, c_int, c_int, c_char_p, c_size_t], c_size_t),
@@ -185,6 +188,8 @@ def set_device(dev): load().ssa_amd_set_device(dev)
 def set_id_offset(off): load().ssa_amd_set_id_offset(off)
 def prepare_db(): return load().ssa_amd_prepare_db()
 def set_option(name, value): load().ssa_amd_set_option(_b(name), value)
+def save_db(path): return load().ssa_amd_save_db(_b(path))
+def load_db(path): return load().ssa_amd_load_db(_b(path))
 
 
 def stats():

@@ -117,10 +117,14 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     const double t0 = now_ms();
     check_width(bw);
     ensure_device_db();
+    const double ta = now_ms();
     R.views = query_views(q);
     SearchScores sc;
+    const double tb = now_ms();
     device_search(R.views, algo, k, bw, sc);
     const double t1 = now_ms();
+    if (trace_on())
+        fprintf(stderr, "trace: ensure %.3f views %.3f device_search %.3f\n", ta - t0, tb - ta, t1 - tb);
     TopK heap(k);
     replay(sc, device_db().meta, R.views, heap, want_log ? &R.hits : nullptr);
     if (!want_log) R.hits = heap.sorted();
@@ -295,6 +299,16 @@ int ssa_amd_prepare_db(void) {
 
 void ssa_amd_get_stats(ssa_amd_stats_t* out) {
     if (out) *out = stats();
+}
+
+int ssa_amd_save_db(const char* path) {
+    if (!path) return 1;
+    return save_packed_db(path);
+}
+
+int ssa_amd_load_db(const char* path) {
+    if (!path) return 1;
+    return load_packed_db(path);
 }
 
 size_t ssa_amd_align_pair(int algo, const char* query, size_t qlen, const char* db, size_t dlen, size_t region[4],

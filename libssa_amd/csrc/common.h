@@ -37,6 +37,9 @@ struct Config {
 };
 Config& cfg();
 
+// SSA_AMD_TRACE=1: per-search host/device timing lines on stderr
+bool trace_on();
+
 // --------------------------------------------------------------- messages
 // Same channels and prefixes as the reference (util.c:36-89): errors and
 // warnings and infos go to stdout gated by the output mode, fatal goes to

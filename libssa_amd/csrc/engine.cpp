@@ -5,6 +5,7 @@
 // re-fetches and re-maps every sequence on every search) and its per-thread
 // SIMD drivers (search_16.c:92-134, search_8.c:94-146).
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -43,11 +44,15 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
     dfree(d_work); dfree(d_smax);
-    dfree(d_cand); dfree(d_cand_score); dfree(d_summary); dfree(d_thresh); dfree(d_fcount);
+    dfree(d_cand); dfree(d_cand_score); dfree(d_summary); dfree(d_thresh); dfree(d_fcount); dfree(d_thresh_local);
     if (h_cand) (void)hipHostFree(h_cand);
     if (h_cand_score) (void)hipHostFree(h_cand_score);
     if (h_fcount) (void)hipHostFree(h_fcount);
+    if (h_up) (void)hipHostFree(h_up);
+    h_up = nullptr;
+    h_up_cap = 0;
     d_cand = nullptr; d_cand_score = nullptr; d_summary = nullptr; d_thresh = nullptr; d_fcount = nullptr;
+    d_thresh_local = nullptr;
     h_cand = nullptr; h_cand_score = nullptr; h_fcount = nullptr; h_cand_cap = 0;
     if (h_scores) (void)hipHostFree(h_scores);
     if (h_ovf) (void)hipHostFree(h_ovf);
@@ -100,15 +105,15 @@ struct Staged {
     EntryMeta meta;
     std::vector<uint64_t> off;       // entry -> offset into codes
     std::vector<uint8_t> codes;
+    std::vector<std::pair<size_t, size_t>> unknown;   // (record, count) with unknown symbols
 };
 
-void stage_from_plugin(Staged& S) {
+// Records [r0, r1) -> entries, as db_adapter.c:47-110 + 212-239 build them.
+void stage_range(size_t r0, size_t r1, Staged& S) {
     const int st = cfg().symtype, strands = cfg().strands;
-    const size_t count = ssa_db_get_sequence_count();
     EntryMeta& M = S.meta;
-    M.records = count;
     std::vector<uint8_t> nt;
-    for (size_t id = 0; id < count; id++) {
+    for (size_t id = r0; id < r1; id++) {
         p_seqinfo si = ssa_db_get_sequence(id);
         if (!si) break;
         if (si->seqlen == 0) continue;
@@ -159,20 +164,145 @@ void stage_from_plugin(Staged& S) {
             S.off.push_back(base);
             M.residues += n;
         }
-        if (unknown > 0) print_warning("%ld unknown symbols found and set to zero", (long)unknown);
+        if (unknown > 0) S.unknown.push_back({id, unknown});
     }
 }
-}  // namespace
 
-void ensure_device_db() {
+unsigned host_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+
+// The plugin is called from several threads at once, as the reference's
+// own search threads do (adp_next_chunk runs in every worker).
+void stage_from_plugin(Staged& S) {
+    const size_t count = ssa_db_get_sequence_count();
+    const unsigned nth = count < 20000 ? 1u : host_threads();
+    std::vector<Staged> part(nth);
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() { stage_range(count * t / nth, count * (t + 1) / nth, part[t]); });
+    for (auto& th : pool) th.join();
+    S.meta.records = count;
+    size_t ne = 0, nc = 0;
+    for (auto& P : part) {
+        ne += P.meta.size();
+        nc += P.codes.size();
+    }
+    S.meta.id.reserve(ne); S.meta.strand.reserve(ne); S.meta.frame.reserve(ne); S.meta.len.reserve(ne);
+    S.off.reserve(ne);
+    S.codes.reserve(nc);
+    for (auto& P : part) {
+        const uint64_t base = S.codes.size();
+        S.meta.id.insert(S.meta.id.end(), P.meta.id.begin(), P.meta.id.end());
+        S.meta.strand.insert(S.meta.strand.end(), P.meta.strand.begin(), P.meta.strand.end());
+        S.meta.frame.insert(S.meta.frame.end(), P.meta.frame.begin(), P.meta.frame.end());
+        S.meta.len.insert(S.meta.len.end(), P.meta.len.begin(), P.meta.len.end());
+        for (uint64_t o : P.off) S.off.push_back(o + base);
+        S.codes.insert(S.codes.end(), P.codes.begin(), P.codes.end());
+        S.meta.residues += P.meta.residues;
+        for (auto& u : P.unknown) print_warning("%ld unknown symbols found and set to zero", (long)u.second);
+        P = Staged();
+    }
+}
+
+// Device layout built on the host; also the on-disk format.
+struct HostPack {
+    EntryMeta meta;
+    std::vector<GroupDesc> groups;
+    std::vector<uint32_t> lane_len, lane_out;
+    std::vector<uint8_t> res;           // blocks * 1 KiB
+    std::vector<uint8_t> code_of;
+    uint64_t blocks = 0;
+};
+
+void build_host_pack(HostPack& H) {
+    Staged S;
+    stage_from_plugin(S);
+    const size_t E = S.meta.size();
+
+    // length-sorted groups of 64 lanes (longest first: long waves start
+    // early); a stable counting sort by length, entry order within a length
+    uint32_t maxlen = 0;
+    for (uint32_t l : S.meta.len) maxlen = std::max(maxlen, l);
+    std::vector<uint32_t> order(E);
+    if (maxlen < (1u << 24)) {
+        std::vector<uint64_t> start((size_t)maxlen + 2, 0);
+        for (uint32_t l : S.meta.len) start[(size_t)(maxlen - l) + 1]++;
+        for (size_t i = 1; i < start.size(); i++) start[i] += start[i - 1];
+        for (uint32_t e = 0; e < E; e++) order[start[maxlen - S.meta.len[e]]++] = e;
+    } else {
+        std::iota(order.begin(), order.end(), 0u);
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return S.meta.len[a] > S.meta.len[b]; });
+    }
+    const uint32_t ngroups = (uint32_t)((E + 63) / 64);
+    H.groups.resize(ngroups);
+    uint64_t blocks = 0;
+    for (uint32_t g = 0; g < ngroups; g++) {
+        const uint32_t longest = S.meta.len[order[(size_t)g * 64]];
+        // columns to compute: longest + 1 (the high half lags one column),
+        // rounded to the 4-column row-buffer quad; residues in 16-column blocks
+        const uint32_t ncols = ((longest + 1) + 3) / 4 * 4;
+        H.groups[g].blk = (uint32_t)blocks;
+        H.groups[g].ncols = ncols;
+        blocks += (ncols + 15) / 16;
+    }
+    if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
+    H.blocks = blocks;
+    const unsigned nth = host_threads();
+    // compact alphabet: the residue codes that occur, in code order; the
+    // padding column gets the next code.  Pair-symbol profiles scale with
+    // (alpha+1)^2, so a 20-letter DB uses 441 rows instead of 1024.
+    std::vector<std::array<uint8_t, 256>> seen(nth);
+    {
+        std::vector<std::thread> pool;
+        const size_t nc = S.codes.size();
+        for (unsigned t = 0; t < nth; t++)
+            pool.emplace_back([&, t]() {
+                seen[t].fill(0);
+                const uint8_t* c = S.codes.data();
+                for (size_t i = nc * t / nth, e = nc * (t + 1) / nth; i < e; i++) seen[t][c[i]] = 1;
+            });
+        for (auto& th : pool) th.join();
+    }
+    uint8_t remap[256] = {0};
+    H.code_of.clear();
+    for (int c = 0; c < 256; c++) {
+        bool any = false;
+        for (auto& v : seen) any |= v[c] != 0;
+        if (any) {
+            remap[c] = (uint8_t)H.code_of.size();
+            H.code_of.push_back((uint8_t)c);
+        }
+    }
+    if (H.code_of.size() > 31) fatal("residue alphabet too large (%d codes)", (int)H.code_of.size());
+    const uint8_t pad = (uint8_t)H.code_of.size();
+    H.lane_len.assign((size_t)ngroups * 64, 0);
+    H.lane_out.assign((size_t)ngroups * 64, 0xffffffffu);
+    H.res.assign((size_t)blocks * 1024, pad);
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nth; t++) {
+        pool.emplace_back([&, t]() {
+            for (uint32_t g = t; g < ngroups; g += nth) {
+                uint8_t* gbase = H.res.data() + (size_t)H.groups[g].blk * 1024;
+                for (uint32_t l = 0; l < 64; l++) {
+                    const size_t pos = (size_t)g * 64 + l;
+                    if (pos >= E) break;
+                    const uint32_t e = order[pos];
+                    const uint32_t n = S.meta.len[e];
+                    H.lane_len[pos] = n;
+                    H.lane_out[pos] = e;
+                    const uint8_t* src = S.codes.data() + S.off[e];
+                    for (uint32_t c = 0; c < n; c++) gbase[(size_t)(c / 16) * 1024 + l * 16 + (c & 15)] = remap[src[c]];
+                }
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    H.meta = std::move(S.meta);
+}
+
+void upload_pack(HostPack& H, int dev) {
     DeviceDB& D = device_db();
     const Config& C = cfg();
-    int dev = C.device;
-    if (dev < 0) check(hipGetDevice(&dev), "hipGetDevice");
-    if (D.generation == C.db_generation && D.device == dev && D.symtype == C.symtype &&
-        D.strands == C.strands && D.dgencode == C.d_gencode)
-        return;
-    const double t0 = now_ms();
     D.release();
     check(hipSetDevice(dev), "hipSetDevice");
     D.device = dev;
@@ -180,83 +310,22 @@ void ensure_device_db() {
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
         for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
     }
-
-    Staged S;
-    stage_from_plugin(S);
-    const size_t E = S.meta.size();
-
-    // length-sorted groups of 64 lanes (longest first: long waves start early)
-    std::vector<uint32_t> order(E);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return S.meta.len[a] > S.meta.len[b]; });
-    const uint32_t ngroups = (uint32_t)((E + 63) / 64);
-    std::vector<GroupDesc> groups(ngroups);
-    uint64_t blocks = 0;
-    for (uint32_t g = 0; g < ngroups; g++) {
-        const uint32_t longest = S.meta.len[order[(size_t)g * 64]];
-        // columns to compute: longest + 1 (the high half lags one column),
-        // rounded to the 4-column row-buffer quad; residues in 16-column blocks
-        const uint32_t ncols = ((longest + 1) + 3) / 4 * 4;
-        groups[g].blk = (uint32_t)blocks;
-        groups[g].ncols = ncols;
-        blocks += (ncols + 15) / 16;
-    }
-    if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
-    // compact alphabet: the residue codes that occur, in code order; the
-    // padding column gets the next code.  Pair-symbol profiles scale with
-    // (alpha+1)^2, so a 20-letter DB uses 441 rows instead of 1024.
-    bool present[256] = {false};
-    for (uint8_t c : S.codes) present[c] = true;
-    std::vector<uint8_t> code_of;
-    uint8_t remap[256] = {0};
-    for (int c = 0; c < 256; c++)
-        if (present[c]) {
-            remap[c] = (uint8_t)code_of.size();
-            code_of.push_back((uint8_t)c);
-        }
-    if (code_of.size() > 31) fatal("residue alphabet too large (%d codes)", (int)code_of.size());
-    const uint8_t pad = (uint8_t)code_of.size();
-    for (auto& c : S.codes) c = remap[c];
-    std::vector<uint32_t> lane_len((size_t)ngroups * 64, 0), lane_out((size_t)ngroups * 64, 0xffffffffu);
-    std::vector<uint8_t> res((size_t)blocks * 1024, pad);
-    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < nth; t++) {
-        pool.emplace_back([&, t]() {
-            for (uint32_t g = t; g < ngroups; g += nth) {
-                uint8_t* gbase = res.data() + (size_t)groups[g].blk * 1024;
-                for (uint32_t l = 0; l < 64; l++) {
-                    const size_t pos = (size_t)g * 64 + l;
-                    if (pos >= E) break;
-                    const uint32_t e = order[pos];
-                    const uint32_t n = S.meta.len[e];
-                    lane_len[pos] = n;
-                    lane_out[pos] = e;
-                    const uint8_t* src = S.codes.data() + S.off[e];
-                    for (uint32_t c = 0; c < n; c += 16)
-                        std::memcpy(gbase + (size_t)(c / 16) * 1024 + l * 16, src + c, std::min(16u, n - c));
-                }
-            }
-        });
-    }
-    for (auto& th : pool) th.join();
-
-    // upload
+    const size_t E = H.meta.size();
     auto dalloc = [&](void** p, size_t bytes, const char* what) {
         check(hipMalloc(p, bytes ? bytes : 16), what);
     };
-    dalloc((void**)&D.d_groups, groups.size() * sizeof(GroupDesc), "groups");
-    dalloc((void**)&D.d_res, res.size(), "residues");
-    dalloc((void**)&D.d_rowbuf, res.size() * 4, "row buffer");
-    dalloc((void**)&D.d_lane_len, lane_len.size() * 4, "lane_len");
-    dalloc((void**)&D.d_lane_out, lane_out.size() * 4, "lane_out");
-    dalloc((void**)&D.d_smax, lane_out.size() * 4, "running max");
+    dalloc((void**)&D.d_groups, H.groups.size() * sizeof(GroupDesc), "groups");
+    dalloc((void**)&D.d_res, H.res.size(), "residues");
+    dalloc((void**)&D.d_rowbuf, H.res.size() * 4, "row buffer");
+    dalloc((void**)&D.d_lane_len, H.lane_len.size() * 4, "lane_len");
+    dalloc((void**)&D.d_lane_out, H.lane_out.size() * 4, "lane_out");
+    dalloc((void**)&D.d_smax, H.lane_out.size() * 4, "running max");
     {
         const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
         dalloc((void**)&D.d_cand, std::max<size_t>(E, 1) * 4, "candidates");
         dalloc((void**)&D.d_cand_score, std::max<size_t>(E, 1) * 4, "candidate scores");
         dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
+        dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
         dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
         dalloc((void**)&D.d_fcount, 16, "filter counters");
         D.h_cand_cap = 1 << 16;
@@ -270,23 +339,146 @@ void ensure_device_db() {
     dalloc((void**)&D.d_matrix, 1024 * 8, "matrix");
     check(hipHostMalloc((void**)&D.h_ovf, (kOvfCap + 1) * 4, hipHostMallocDefault), "pinned");
     check(hipHostMalloc((void**)&D.h_wide, kOvfCap * 8, hipHostMallocDefault), "pinned");
-    check(hipMemcpy(D.d_groups, groups.data(), groups.size() * sizeof(GroupDesc), hipMemcpyHostToDevice), "H2D");
-    check(hipMemcpy(D.d_res, res.data(), res.size(), hipMemcpyHostToDevice), "H2D residues");
-    check(hipMemcpy(D.d_lane_len, lane_len.data(), lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
-    check(hipMemcpy(D.d_lane_out, lane_out.data(), lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
-    D.ngroups = ngroups;
-    D.nblocks = blocks;
-    D.len_sorted = S.meta.len;
+    check(hipMemcpy(D.d_groups, H.groups.data(), H.groups.size() * sizeof(GroupDesc), hipMemcpyHostToDevice), "H2D");
+    check(hipMemcpy(D.d_res, H.res.data(), H.res.size(), hipMemcpyHostToDevice), "H2D residues");
+    check(hipMemcpy(D.d_lane_len, H.lane_len.data(), H.lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
+    check(hipMemcpy(D.d_lane_out, H.lane_out.data(), H.lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
+    D.ngroups = (uint32_t)H.groups.size();
+    D.nblocks = H.blocks;
+    D.len_sorted = H.meta.len;
     std::sort(D.len_sorted.begin(), D.len_sorted.end());
-    D.meta = std::move(S.meta);
-    D.lane_out = std::move(lane_out);
-    D.code_of = std::move(code_of);
-    D.alpha = pad;
+    D.meta = std::move(H.meta);
+    D.lane_out = std::move(H.lane_out);
+    D.code_of = std::move(H.code_of);
+    D.alpha = (uint32_t)D.code_of.size();
     D.generation = C.db_generation;
     D.symtype = C.symtype;
     D.strands = C.strands;
     D.dgencode = C.d_gencode;
+}
+
+int current_device() {
+    int dev = cfg().device;
+    if (dev < 0) check(hipGetDevice(&dev), "hipGetDevice");
+    return dev;
+}
+
+// ------------------------------------------------------ packed DB files
+// "SSAPACK1" | u32 version, symtype, strands, dgencode | u64 records,
+// entries, residues, ngroups, blocks | u32 alpha, 0 | u8 code_of[32] |
+// u64 id[E] | u8 strand[E] | u8 frame[E] | u32 len[E] | GroupDesc[ngroups]
+// | u32 lane_len[64 ngroups] | u32 lane_out[64 ngroups] | u8 res[1 KiB * blocks]
+constexpr char kPackMagic[8] = {'S', 'S', 'A', 'P', 'A', 'C', 'K', '1'};
+constexpr uint32_t kPackVersion = 1;
+
+template <class T>
+bool wr(FILE* f, const T* p, size_t n) { return n == 0 || fwrite(p, sizeof(T), n, f) == n; }
+template <class T>
+bool rd(FILE* f, T* p, size_t n) { return n == 0 || fread(p, sizeof(T), n, f) == n; }
+
+}  // namespace
+
+void ensure_device_db() {
+    DeviceDB& D = device_db();
+    const Config& C = cfg();
+    const int dev = current_device();
+    if (D.generation == C.db_generation && D.device == dev && D.symtype == C.symtype &&
+        D.strands == C.strands && D.dgencode == C.d_gencode)
+        return;
+    const double t0 = now_ms();
+    check(hipSetDevice(dev), "hipSetDevice");
+    HostPack H;
+    build_host_pack(H);
+    upload_pack(H, dev);
     stats().pack_ms = now_ms() - t0;
+}
+
+int save_packed_db(const char* path) {
+    ensure_device_db();
+    DeviceDB& D = device_db();
+    FILE* f = fopen(path, "wb");
+    if (!f) {
+        print_error("Cannot open packed DB file for writing: %s", path);
+        return 1;
+    }
+    const uint64_t E = D.meta.size();
+    std::vector<uint8_t> res((size_t)D.nblocks * 1024);
+    std::vector<GroupDesc> groups(D.ngroups);
+    std::vector<uint32_t> lane_len((size_t)D.ngroups * 64);
+    check(hipSetDevice(D.device), "hipSetDevice");
+    check(hipMemcpy(res.data(), D.d_res, res.size(), hipMemcpyDeviceToHost), "D2H residues");
+    check(hipMemcpy(groups.data(), D.d_groups, groups.size() * sizeof(GroupDesc), hipMemcpyDeviceToHost), "D2H");
+    check(hipMemcpy(lane_len.data(), D.d_lane_len, lane_len.size() * 4, hipMemcpyDeviceToHost), "D2H");
+    const uint32_t hdr32[4] = {kPackVersion, (uint32_t)D.symtype, (uint32_t)D.strands, (uint32_t)D.dgencode};
+    const uint64_t hdr64[5] = {(uint64_t)D.meta.records, E, D.meta.residues, D.ngroups, D.nblocks};
+    const uint32_t alpha[2] = {D.alpha, 0};
+    uint8_t code_of[32] = {0};
+    std::copy(D.code_of.begin(), D.code_of.end(), code_of);
+    bool ok = wr(f, kPackMagic, 8) && wr(f, hdr32, 4) && wr(f, hdr64, 5) && wr(f, alpha, 2) && wr(f, code_of, 32) &&
+              wr(f, D.meta.id.data(), E) && wr(f, D.meta.strand.data(), E) && wr(f, D.meta.frame.data(), E) &&
+              wr(f, D.meta.len.data(), E) && wr(f, groups.data(), groups.size()) &&
+              wr(f, lane_len.data(), lane_len.size()) && wr(f, D.lane_out.data(), D.lane_out.size()) &&
+              wr(f, res.data(), res.size());
+    ok = (fclose(f) == 0) && ok;
+    if (!ok) print_error("Writing packed DB file failed: %s", path);
+    return ok ? 0 : 1;
+}
+
+int load_packed_db(const char* path) {
+    const Config& C = cfg();
+    FILE* f = fopen(path, "rb");
+    if (!f) {
+        print_error("Cannot open packed DB file: %s", path);
+        return 1;
+    }
+    char magic[8];
+    uint32_t hdr32[4], alpha[2];
+    uint64_t hdr64[5];
+    uint8_t code_of[32];
+    HostPack H;
+    auto fail = [&](const char* why) {
+        fclose(f);
+        print_error("Packed DB file %s: %s", path, why);
+        return 1;
+    };
+    if (!rd(f, magic, 8) || memcmp(magic, kPackMagic, 8) || !rd(f, hdr32, 4) || !rd(f, hdr64, 5) ||
+        !rd(f, alpha, 2) || !rd(f, code_of, 32))
+        return fail("not a packed DB");
+    if (hdr32[0] != kPackVersion) return fail("unsupported version");
+    if ((int)hdr32[1] != C.symtype || (int)hdr32[2] != C.strands || (int)hdr32[3] != C.d_gencode)
+        return fail("packed for another symbol type / strands / genetic code");
+    if (hdr64[0] != ssa_db_get_sequence_count()) return fail("record count differs from the open DB");
+    const uint64_t E = hdr64[1], ng = hdr64[3];
+    if (alpha[0] > 31 || E > ng * 64 || ng > E / 64 + 1) return fail("corrupt header");
+    H.meta.records = hdr64[0];
+    H.meta.residues = hdr64[2];
+    H.blocks = hdr64[4];
+    H.code_of.assign(code_of, code_of + alpha[0]);
+    H.meta.id.resize(E); H.meta.strand.resize(E); H.meta.frame.resize(E); H.meta.len.resize(E);
+    H.groups.resize(ng);
+    H.lane_len.resize(ng * 64);
+    H.lane_out.resize(ng * 64);
+    H.res.resize(H.blocks * 1024);
+    if (!rd(f, H.meta.id.data(), E) || !rd(f, H.meta.strand.data(), E) || !rd(f, H.meta.frame.data(), E) ||
+        !rd(f, H.meta.len.data(), E) || !rd(f, H.groups.data(), ng) || !rd(f, H.lane_len.data(), ng * 64) ||
+        !rd(f, H.lane_out.data(), ng * 64) || !rd(f, H.res.data(), H.res.size()))
+        return fail("truncated");
+    fclose(f);
+    // structural checks before anything reaches the device
+    for (uint64_t g = 0; g < ng; g++) {
+        const GroupDesc& G = H.groups[g];
+        if ((uint64_t)G.blk + (G.ncols + 15) / 16 > H.blocks || G.ncols % 4) return fail("corrupt group table");
+        for (int l = 0; l < 64; l++) {
+            const uint32_t o = H.lane_out[g * 64 + l];
+            if (o != 0xffffffffu && (o >= E || H.lane_len[g * 64 + l] != H.meta.len[o] ||
+                                     H.lane_len[g * 64 + l] + 1 > G.ncols))
+                return fail("corrupt lane table");
+        }
+    }
+    const double t0 = now_ms();
+    upload_pack(H, current_device());
+    stats().pack_ms = now_ms() - t0;
+    return 0;
 }
 
 // ----------------------------------------------------------------- search
@@ -364,7 +556,8 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
     out.dev_o8 = out.dev_o16 = 0;
     // single query view and a small k: only heap-changing candidates come back
     const double t_prep0 = now_ms();
-    double prep = 0;
+    double prep = 0, sync_wait = 0;
+    float upload = 0;
     out.sparse = V == 1 && k > 0 && k <= (size_t)kFilterMaxK && E > 0 && views[0].len > 0 && !cfg().no_filter;
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
@@ -498,9 +691,24 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
             D.work_cap = (size_t)wide_threads * 2 * m;
         }
         hipStream_t st = D.stream;
-        check(hipMemcpyAsync(D.d_qpt, qpt.data(), qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
-        check(hipMemcpyAsync(D.d_query, qv.seq, m, hipMemcpyHostToDevice, st), "H2D query");
-        check(hipMemcpyAsync(D.d_matrix, Mc, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        // one pinned staging buffer for the per-search uploads (pageable
+        // sources would make each copy a synchronous staged transfer)
+        const size_t up_bytes = qpt.size() * 4 + 1024 * 8 + ((m + 15) & ~(size_t)15);
+        if (D.h_up_cap < up_bytes) {
+            if (D.h_up) (void)hipHostFree(D.h_up);
+            check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
+            D.h_up_cap = up_bytes;
+        }
+        uint8_t* up_q = D.h_up;
+        uint8_t* up_m = up_q + qpt.size() * 4;
+        uint8_t* up_s = up_m + 1024 * 8;
+        memcpy(up_q, qpt.data(), qpt.size() * 4);
+        memcpy(up_m, Mc, 1024 * 8);
+        memcpy(up_s, qv.seq, m);
+        check(hipEventRecord(D.ev[4], st), "event");
+        check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+        check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
+        check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
         check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
 
         StripArgs a{};
@@ -571,6 +779,7 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
             f.bw = bw;
             f.summary = D.d_summary;
             f.thresh = D.d_thresh;
+            f.thresh_local = D.d_thresh_local;
             f.cand = D.d_cand;
             f.cand_score = D.d_cand_score;
             f.counters = D.d_fcount;
@@ -588,7 +797,27 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
         check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
         check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
         check(hipEventRecord(D.ev[3], st), "event");
+        const double t_sync0 = now_ms();
+        if (trace_on()) {
+            const double a0 = now_ms();
+            check(hipEventSynchronize(D.ev[4]), "ev");
+            const double a1 = now_ms();
+            check(hipEventSynchronize(D.ev[0]), "ev");
+            const double a2 = now_ms();
+            check(hipEventSynchronize(D.ev[1]), "ev");
+            const double a3 = now_ms();
+            fprintf(stderr, "trace: enqueue %.3f  ev4 +%.3f ev0 +%.3f ev1 +%.3f (from sync start)\n",
+                    t_sync0 - (t_prep0 + prep), a1 - a0, a2 - a0, a3 - a0);
+        }
         check(hipStreamSynchronize(st), "search");
+        sync_wait += now_ms() - t_sync0;
+        const double t_post0 = now_ms();
+
+        {
+            float u;
+            check(hipEventElapsedTime(&u, D.ev[4], D.ev[0]), "elapsed");
+            upload += u;
+        }
         if (out.sparse) {
             const uint32_t nc = D.h_fcount[0];
             if (nc > D.h_cand_cap) {
@@ -624,12 +853,17 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
         wms += t;
         check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
         dms += t;
+        if (trace_on()) fprintf(stderr, "trace: post-sync %.3f\n", now_ms() - t_post0);
         // algorithmic bytes: residues once + per-entry score write + profile
         kernel_bytes += D.meta.residues + 4ull * E + qpt.size() * 4;
     }
+    if (trace_on())
+        fprintf(stderr, "trace: prep %.3f sync %.3f total %.3f\n", prep, sync_wait, now_ms() - t_prep0);
     ssa_amd_stats_t& S = stats();
     S.kernel_ms = kms;
     S.prep_ms = V == 1 ? prep : 0;
+    S.upload_ms = upload;
+    S.sync_wait_ms = sync_wait;
     S.wide_ms = wms;
     S.d2h_ms = dms;
     S.cells = out.cells;

@@ -43,11 +43,14 @@ struct DeviceDB {
     int32_t* d_cand_score = nullptr;
     int32_t* d_summary = nullptr;
     int32_t* d_thresh = nullptr;
+    int32_t* d_thresh_local = nullptr;
     uint32_t* d_fcount = nullptr;
     uint32_t* h_cand = nullptr;           // pinned, h_cand_cap entries
     int32_t* h_cand_score = nullptr;
     uint32_t* h_fcount = nullptr;
     size_t h_cand_cap = 0;
+    uint8_t* h_up = nullptr;              // pinned staging for per-search uploads
+    size_t h_up_cap = 0;
     int32_t* d_scores = nullptr;
     int32_t* h_scores = nullptr;          // pinned, [views][entries]
     size_t h_scores_cap = 0;
@@ -72,6 +75,8 @@ struct DeviceDB {
 };
 DeviceDB& device_db();
 void ensure_device_db();                  // (re)packs from the plugin when stale
+int save_packed_db(const char* path);     // 0 on success
+int load_packed_db(const char* path);     // 0 on success; replaces packing from the plugin
 std::vector<uint8_t> fetch_entry_codes(uint64_t local_id, int strand, int frame);
 
 // Exact scores of every entry for every query view.  Scores live in the

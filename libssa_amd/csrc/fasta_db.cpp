@@ -7,11 +7,21 @@
 // keep their residues as ASCII with line breaks and other whitespace removed;
 // empty records stay (seqlen 0) so later IDs do not shift.
 //
-// The file is read with one sequential pass into a single residue arena; for
-// a 10 M-record shard that is a few seconds, once per init_db.
+// The file is memory-mapped and parsed in parallel: it is cut into one
+// piece per thread at record starts ("\n>"), each piece is parsed into its
+// own residue arena, and the arenas are concatenated in order -- the result
+// is byte-identical to a sequential pass.  A 10 M-record shard takes well
+// under a second per init_db.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "libssa_extern_db.h"
@@ -20,46 +30,106 @@ namespace {
 struct FastaDB {
     std::vector<char> arena;
     std::vector<seqinfo_t> recs;
-    std::vector<size_t> offs;
 };
 FastaDB* g_db = nullptr;
 
-bool load(const char* path, FastaDB& db) {
-    FILE* f = fopen(path, "rb");
-    if (!f) return false;
-    if (fseek(f, 0, SEEK_END) != 0) { fclose(f); return false; }
-    const long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    std::vector<char> buf(sz > 0 ? (size_t)sz : 0);
-    if (sz > 0 && fread(buf.data(), 1, (size_t)sz, f) != (size_t)sz) { fclose(f); return false; }
-    fclose(f);
-    db.arena.reserve(buf.size());
-    const char* p = buf.data();
-    const char* end = p + buf.size();
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+// Parses [p, end): records start at '>' at a line start; residues of the
+// lines that follow a header, whitespace dropped.  Text before the first
+// header is ignored.  `first_in_record` is set when the piece starts inside
+// a record (never: pieces are cut at record starts, except piece 0).
+struct Piece {
+    std::vector<char> res;
+    std::vector<size_t> offs;   // record starts in res
+};
+
+void parse_piece(const char* p, const char* end, bool at_line_start, Piece& out) {
     bool in_rec = false;
     while (p < end) {
         const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
         const char* le = nl ? nl : end;
-        if (*p == '>') {
-            db.offs.push_back(db.arena.size());
+        if (at_line_start && *p == '>') {
+            out.offs.push_back(out.res.size());
             in_rec = true;
         } else if (in_rec) {
-            for (const char* q = p; q < le; q++) {
-                const char c = *q;
-                if (c != ' ' && c != '\t' && c != '\r' && c != '\v' && c != '\f') db.arena.push_back(c);
-            }
+            const size_t base = out.res.size();
+            out.res.resize(base + (size_t)(le - p));
+            char* w = out.res.data() + base;
+            for (const char* q = p; q < le; q++)
+                if (!is_space(*q)) *w++ = *q;
+            out.res.resize((size_t)(w - out.res.data()));
         }
+        at_line_start = true;
         p = nl ? nl + 1 : end;
     }
-    db.offs.push_back(db.arena.size());
-    db.arena.push_back(0);
-    const size_t n = db.offs.size() - 1;
-    db.recs.resize(n);
-    for (size_t i = 0; i < n; i++) {
-        db.recs[i].ID = i;
-        db.recs[i].seqlen = db.offs[i + 1] - db.offs[i];
-        db.recs[i].seq = db.arena.data() + db.offs[i];
+}
+
+bool load(const char* path, FastaDB& db) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return false;
+    struct stat stt;
+    if (fstat(fd, &stt) != 0) { close(fd); return false; }
+    const size_t sz = (size_t)stt.st_size;
+    const char* buf = nullptr;
+    if (sz > 0) {
+        void* m = mmap(nullptr, sz, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { close(fd); return false; }
+        madvise(m, sz, MADV_SEQUENTIAL);
+        buf = (const char*)m;
     }
+    close(fd);
+    const char* end = buf + sz;
+    // cut points at record starts
+    const unsigned nth = sz < (8u << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<const char*> cut{buf};
+    for (unsigned t = 1; t < nth; t++) {
+        const char* c = std::max(cut.back(), buf + sz / nth * t);
+        const char* q = c;
+        while (q < end) {
+            const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+            if (!nl || nl + 1 >= end) { q = end; break; }
+            if (nl[1] == '>') { q = nl + 1; break; }
+            q = nl + 1;
+        }
+        cut.push_back(q);
+    }
+    cut.push_back(end);
+    std::vector<Piece> pieces(nth);
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() {
+            if (cut[t] < cut[t + 1]) parse_piece(cut[t], cut[t + 1], true, pieces[t]);
+        });
+    for (auto& th : pool) th.join();
+    if (buf) munmap((void*)buf, sz);
+    // concatenate
+    size_t total = 0, nrec = 0;
+    std::vector<size_t> rbase(nth), obase(nth);
+    for (unsigned t = 0; t < nth; t++) {
+        rbase[t] = total;
+        obase[t] = nrec;
+        total += pieces[t].res.size();
+        nrec += pieces[t].offs.size();
+    }
+    db.arena.resize(total + 1);
+    db.recs.resize(nrec);
+    pool.clear();
+    for (unsigned t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() {
+            const Piece& P = pieces[t];
+            if (!P.res.empty()) memcpy(db.arena.data() + rbase[t], P.res.data(), P.res.size());
+            for (size_t i = 0; i < P.offs.size(); i++) {
+                const size_t b = P.offs[i];
+                const size_t e = i + 1 < P.offs.size() ? P.offs[i + 1] : P.res.size();
+                seqinfo_t& r = db.recs[obase[t] + i];
+                r.ID = obase[t] + i;
+                r.seqlen = e - b;
+                r.seq = db.arena.data() + rbase[t] + b;
+            }
+        });
+    for (auto& th : pool) th.join();
+    db.arena[total] = 0;
     return true;
 }
 }  // namespace

@@ -58,19 +58,19 @@ struct WideArgs {
 };
 
 // Device-side top-k candidate filter (single query view, k <= kFilterMaxK).
-// Block b of kFilterBlock consecutive entries (insertion order) gets as
-// threshold T[b] the k-th largest of the earlier blocks' maxima -- a lower
-// bound of the reference heap's root whenever one of its entries is
-// offered -- and only entries with score > T[b] (or overflowed, INT32_MIN)
-// can change the heap.  They are compacted into cand[] for the host replay.
+// Every entry gets a lower bound of the reference heap's root at the time
+// it is offered (k-th largest of maxima of earlier 64-entry runs, see
+// kernels.hip); only entries above it (or overflowed, INT32_MIN) can change
+// the heap.  They are compacted into cand[] for the host replay.
 constexpr int kFilterBlock = 4096;
 constexpr int kFilterMaxK = 64;
 struct FilterArgs {
     const int32_t* scores;     // [n] per-entry scores, INT32_MIN = overflowed (exact value elsewhere)
     uint32_t n, k, nblocks;
     int32_t nw, bw;            // counters follow the reference's overflow rules
-    int32_t* summary;          // [nblocks] block maxima
-    int32_t* thresh;           // [nblocks]
+    int32_t* summary;          // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
+    int32_t* thresh;           // [nblocks] bound from earlier blocks
+    int32_t* thresh_local;     // [nblocks * 64] bound from earlier minis of the same block
     uint32_t* cand;            // [n] candidate entry indices (unordered)
     int32_t* cand_score;       // [n] their scores
     uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows

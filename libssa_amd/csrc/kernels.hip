@@ -719,72 +719,96 @@ __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
 // of every score: the reference heap (minheap.c:50-106) rejects an element
 // unless it is not full or the score beats its root, and after any prefix
 // of the insertion order its root is the k-th largest score of that prefix
-// (ties change which IDs it holds, never the score multiset).  Any subset of
-// the prefix gives a lower bound of that root; the filter uses the subset
-// made of each earlier block's maximum: T[b] = k-th largest of
-// {max(block b') : b' < b} (INT32_MIN while there are fewer than k).
-// Overflowed entries are left out of the maxima (that only lowers the bound)
-// and always forwarded.
+// (ties change which IDs it holds, never the score multiset).  The k-th
+// largest of any subset of the prefix is a lower bound of that root; the
+// filter uses the maxima of 64-entry "minis": for an entry in mini m of
+// block b the bound is the larger of
+//   T_local[m] = k-th largest max of the earlier minis of block b,
+//   T_block[b] = k-th largest max of all minis of blocks < b
+// (INT32_MIN while fewer than k).  Overflowed entries are left out of the
+// maxima (that only lowers the bounds) and always forwarded.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) filter_block_max(const FilterArgs a) {
-    __shared__ int32_t wmax[4];
+__device__ __forceinline__ int32_t wave_max(int32_t x) {
+    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
+    return x;
+}
+
+// Inserts x into a descending list held one element per lane (lanes < K),
+// dropping the smallest.  Chain: compare, ballot count, DPP wave_shr:1
+// (a GFX9 DPP mode), select.
+__device__ __forceinline__ int32_t insert_desc(int32_t run, int32_t x, int lane, int K) {
+    const int pos = __popcll(__ballot(lane < K && run >= x));
+    const int32_t up = __builtin_amdgcn_update_dpp(run, run, 0x138, 0xf, 0xf, false);
+    return lane < pos ? run : (lane == pos ? x : up);
+}
+
+constexpr int kMini = 64;
+constexpr int kMinisPerBlock = kFilterBlock / kMini;   // 64
+
+__global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
+    __shared__ int32_t mini_max[kMinisPerBlock];
     __shared__ uint32_t c8, c16;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * kFilterBlock;
     if (threadIdx.x == 0) c8 = c16 = 0;
     __syncthreads();
     uint32_t my8 = 0, my16 = 0;
-    int32_t mx = INT32_MIN;
-    for (int i = threadIdx.x; i < kFilterBlock; i += 256) {
-        const uint32_t e = base + i;
-        if (e >= a.n) break;
-        const int32_t x = a.scores[e];
-        if (x == INT32_MIN) continue;
-        mx = max(mx, x);
-        if (!a.nw) {
-            my8 += a.bw == 8 && x >= 255;
-            my16 += x >= 65535;
-        } else {
-            my8 += a.bw == 8 && (x <= -128 || x >= 127);
-            my16 += x <= -32768 || x >= 32767;
+    for (int i = 0; i < kMinisPerBlock / 4; i++) {
+        const int m = i * 4 + wave;                 // this wave's mini: 64 consecutive entries
+        const uint32_t e = base + m * kMini + lane;
+        const int32_t x = e < a.n ? a.scores[e] : INT32_MIN;
+        if (x != INT32_MIN) {
+            if (!a.nw) {
+                my8 += a.bw == 8 && x >= 255;
+                my16 += x >= 65535;
+            } else {
+                my8 += a.bw == 8 && (x <= -128 || x >= 127);
+                my16 += x <= -32768 || x >= 32767;
+            }
         }
+        const int32_t mx = wave_max(x);
+        if (lane == 0) mini_max[m] = mx;
     }
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
     if (my8) atomicAdd(&c8, my8);
     if (my16) atomicAdd(&c16, my16);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        a.summary[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-        if (c8) atomicAdd(&a.counters[1], c8);
-        if (c16) atomicAdd(&a.counters[2], c16);
+    if (wave == 0) {
+        const int K = (int)a.k;
+        const int32_t mine = mini_max[lane];
+        int32_t run = INT32_MIN, tl = INT32_MIN;
+        for (int m = 0; m < kMinisPerBlock; m++) {
+            const int32_t t = __builtin_amdgcn_readlane(run, K - 1);
+            tl = lane == m ? t : tl;
+            run = insert_desc(run, __builtin_amdgcn_readlane(mine, m), lane, K);
+        }
+        a.thresh_local[(size_t)blockIdx.x * kMinisPerBlock + lane] = tl;
+        a.summary[(size_t)blockIdx.x * kFilterMaxK + lane] = lane < K ? run : INT32_MIN;
+        if (lane == 0) {
+            if (c8) atomicAdd(&a.counters[1], c8);
+            if (c16) atomicAdd(&a.counters[2], c16);
+        }
     }
 }
 
-// One wave keeps the k largest block maxima seen so far (lane i = i-th
-// largest, descending) and inserts one block maximum per step.
+// One wave: running top-k over the block summaries (descending, one per
+// lane).  Merge = bitonic: max(run[i], blk[63-i]) holds the 64 largest of
+// the union as a bitonic sequence, six compare-exchange stages sort it.
 __global__ void __launch_bounds__(64) filter_prefix(const FilterArgs a) {
     const int lane = threadIdx.x;
     const int K = (int)a.k;
     int32_t run = INT32_MIN;
-    int32_t next = lane < (int)a.nblocks ? a.summary[lane] : INT32_MIN;
-    for (uint32_t b0 = 0; b0 < a.nblocks; b0 += 64) {
-        // 64 block maxima per round, one per lane; the next round's are in flight
-        const int32_t xs = next;
-        const uint32_t nb = min(64u, a.nblocks - b0);
-        next = b0 + 64 + lane < a.nblocks ? a.summary[b0 + 64 + lane] : INT32_MIN;
-        int32_t tv = INT32_MIN;
-        for (uint32_t i = 0; i < nb; i++) {
-            // the chain per block: compare, ballot count, wave shift (DPP
-            // wave_shr:1, a GFX9 DPP mode), select -- no memory round trip
-            const int32_t t = __builtin_amdgcn_readlane(run, K - 1);
-            tv = lane == (int)i ? t : tv;
-            const int32_t x = __builtin_amdgcn_readlane(xs, i);
-            // insert x after the entries >= x
-            const int pos = __popcll(__ballot(lane < K && run >= x));
-            const int32_t up = __builtin_amdgcn_update_dpp(run, run, 0x138, 0xf, 0xf, false);
-            run = lane < pos ? run : (lane == pos ? x : up);
+    int32_t nxt = a.nblocks ? a.summary[lane] : INT32_MIN;
+    for (uint32_t b = 0; b < a.nblocks; b++) {
+        const int32_t blk = nxt;
+        if (b + 1 < a.nblocks) nxt = a.summary[(size_t)(b + 1) * kFilterMaxK + lane];
+        const int32_t t = __builtin_amdgcn_readlane(run, K - 1);
+        if (lane == 0) a.thresh[b] = t;
+        int32_t v = max(run, __shfl(blk, 63 - lane));
+        for (int j = 32; j > 0; j >>= 1) {
+            const int32_t o = __shfl_xor(v, j);
+            v = (lane & j) ? min(v, o) : max(v, o);
         }
-        if (lane < (int)nb) a.thresh[b0 + lane] = tv;
+        run = lane < K ? v : INT32_MIN;
     }
 }
 
@@ -792,7 +816,7 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     if (e >= a.n) return;
     const int32_t x = a.scores[e];
-    const int32_t t = a.thresh[e / kFilterBlock];
+    const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
     if (x == INT32_MIN || x > t) {
         const uint32_t i = atomicAdd(&a.counters[0], 1u);
         a.cand[i] = e;
@@ -802,7 +826,7 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
 
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(filter_block_max, dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(filter_block, dim3(a.nblocks), dim3(256), 0, st, a);
     hipLaunchKernelGGL(filter_prefix, dim3(1), dim3(64), 0, st, a);
     hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
     return hipGetLastError();

@@ -16,6 +16,11 @@ Config& cfg() {
 }
 
 // ---------------------------------------------------------------- messages
+bool trace_on() {
+    static const bool on = getenv("SSA_AMD_TRACE") != nullptr;
+    return on;
+}
+
 void fatal(const char* fmt, ...) {
     if (fmt) {
         va_list ap;

@@ -185,3 +185,21 @@ def test_replay_entry_point_is_host_only():
     ids = np.arange(5000, dtype=np.uint64)
     for k in (1, 3, 10, 100, 6000):
         assert S.replay(list(zip(sc.tolist(), ids.tolist())), k) == po.topk(sc, ids, k)
+
+
+def test_packed_db_refuses_foreign_files(tmp_path):
+    """ssa_amd_load_db checks magic, version and settings before any device
+    work (so this runs without a GPU)."""
+    import libssa_amd as S
+    S.set_output_mode(S.OUTPUT_SILENT)
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+    bad = tmp_path / "bad.ssapack"
+    bad.write_bytes(b"NOTAPACK" + bytes(200))
+    assert S.load_db(str(bad)) != 0
+    assert S.load_db(str(tmp_path / "missing.ssapack")) != 0
+    import struct
+    hdr = b"SSAPACK1" + struct.pack("<4I", 1, S.NUCLEOTIDE, 1, 1) + struct.pack("<5Q", 0, 0, 0, 0, 0) + bytes(40)
+    other = tmp_path / "other.ssapack"
+    other.write_bytes(hdr)
+    assert S.load_db(str(other)) != 0
+    S.set_output_mode(S.OUTPUT_WARNING)

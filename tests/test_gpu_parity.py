@@ -520,3 +520,44 @@ def test_device_topk_filter_matches_full_scan(pattern):
             S.set_option("no_filter", 0)
             assert S.search(qq, algo, 7, 16, S.LOG) == log_full
         S.free_sequence(qq)
+
+
+def test_packed_db_save_load_roundtrip(tmp_path):
+    """ssa_amd_save_db / ssa_amd_load_db: a reloaded packed DB gives the same
+    results as packing from the plugin (protein, and NUCLEOTIDE with both
+    strands = two entries per record), and a file packed under other
+    settings is refused."""
+    q = syn.protein_query(120, 4)
+    codes, off = syn.protein_db(5000, 8, query=q, plant_every=500, lo=1, hi=600)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    path = _write_db(str(tmp_path), codes, off)
+    S.init_db(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    ref = {k: [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)] for k in (5, 100)}
+    ref_nw = [(h["score"], h["id"]) for h in S.nw_align(qq, 50, 16)]
+    pk = str(tmp_path / "db.ssapack")
+    assert S.save_db(pk) == 0
+    S.init_db(path)                 # new generation: would repack from the plugin
+    assert S.load_db(pk) == 0
+    for k in (5, 100):
+        assert [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)] == ref[k]
+    assert [(h["score"], h["id"]) for h in S.nw_align(qq, 50, 16)] == ref_nw
+    S.free_sequence(qq)
+    # refused: other symbol type
+    S.init_symbol_translation(S.NUCLEOTIDE, S.BOTH_STRANDS, 1, 1)
+    S.init_db(path)
+    assert S.load_db(pk) != 0
+    # NUCLEOTIDE both strands round trip
+    seqs = po.read_fasta(os.path.join(DATA, "AF091148.fas"))[:400]
+    configure(True, ("const", 2, -3), -5, -2, strands=S.BOTH_STRANDS)
+    S.init_db(os.path.join(DATA, "AF091148.fas"))
+    qn = S.init_sequence_fasta(S.READ_FROM_FILE, os.path.join(DATA, "one_seq.fas"))
+    ref = [(h["score"], h["id"], h["db_strand"]) for h in S.sw_align(qn, 40, 16)]
+    pk2 = str(tmp_path / "nt.ssapack")
+    assert S.save_db(pk2) == 0
+    S.init_db(os.path.join(DATA, "AF091148.fas"))
+    assert S.load_db(pk2) == 0
+    assert [(h["score"], h["id"], h["db_strand"]) for h in S.sw_align(qn, 40, 16)] == ref
+    S.free_sequence(qn)
+    del seqs
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
