@@ -34,6 +34,7 @@ struct Config {
     int force_wide = 0;                   // 1: score everything with the int64 kernel
     int sw_kernel = 0;                    // 0: f16-pattern kernel when applicable, 1: int16 kernel
     int no_filter = 0;                    // 1: copy every score back (no device top-k filter)
+    int pair_np = 24;                     // pair kernel main strip: 24 (48 rows, default) or 16 (32 rows)
 };
 Config& cfg();
 

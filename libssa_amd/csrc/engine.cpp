@@ -592,7 +592,9 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
         // SW on f16 bit patterns needs non-positive gaps and scores within
         // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
         const uint32_t prow = A + 1;
-        const size_t pair_lds = (size_t)prow * prow * (np + 4) * 4;
+        // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
+        const int pnp = C.pair_np == 24 ? 24 : 16;
+        const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
         // NW on f16 patterns: only when no more than a handful of entries
         // exceed its length bound (those are re-scored by the int64 kernel)
         uint32_t nw_base = 0, nmax_f16 = 0;
@@ -617,7 +619,7 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
         const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
         // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
         // rows up to the last strip's end so table builders need no bounds test
-        const size_t mpad = (size_t)nstrips * 2 * np + 64;
+        const size_t mpad = std::max<size_t>((size_t)nstrips * 2 * np, m + 2 * pnp) + 64;
         std::vector<uint16_t> P((size_t)(A + 1) * mpad, (uint16_t)padv);
         for (uint32_t c = 0; c < A; c++) {
             const int64_t* row = M + ((size_t)D.code_of[c] << 5);
@@ -631,11 +633,21 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
         std::vector<PairLaunch> plan;
         std::vector<uint32_t> qpt;
         if (use_pair) {
-            // 32-row strips; a remainder of <= 16 rows becomes one 16-row
-            // (NP = 8) strip; NW's last strip runs as its own capture launch
-            const uint32_t full = (uint32_t)(m / 32), rem = (uint32_t)(m % 32);
-            const bool tail = rem > 0 && rem <= 16;
-            const uint32_t nmain = tail || rem == 0 ? full : full + 1;
+            // main strips of 2*pnp rows; the remainder becomes one strip of
+            // the smallest height that holds it (16 rows: NP 8, 32: NP 16);
+            // NW's last strip runs as its own capture launch
+            const uint32_t Hm = 2 * pnp;
+            const uint32_t full = (uint32_t)(m / Hm), rem = (uint32_t)(m % Hm);
+            std::vector<std::pair<int, uint32_t>> segs;   // (np, strips)
+            if (rem == 0) segs = {{pnp, full}};
+            else if (rem <= 16) segs = {{pnp, full}, {8, 1}};
+            else if (rem <= 32 && pnp > 16) segs = {{pnp, full}, {16, 1}};
+            else segs = {{pnp, full + 1}};
+            if (nw && segs.back().second > 1) {
+                const int snp = segs.back().first;
+                segs.back().second--;
+                segs.push_back({snp, 1});
+            }
             auto add_tables = [&](int Ph, uint32_t row0, uint32_t count) {
                 const size_t off = qpt.size();
                 qpt.resize(off + (size_t)count * prow * prow * Ph);
@@ -652,10 +664,14 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
                 }
                 return off;
             };
-            const uint32_t nbulk = nw && !tail ? nmain - 1 : nmain;
-            if (nbulk > 0) plan.push_back({16, 0, nbulk, add_tables(16, 0, nbulk), 0, false});
-            if (tail) plan.push_back({8, full * 32, 1, add_tables(8, full * 32, 1), 0, nw});
-            else if (nw) plan.push_back({16, nbulk * 32, 1, add_tables(16, nbulk * 32, 1), 0, true});
+            uint32_t row0 = 0;
+            for (size_t g = 0; g < segs.size(); g++) {
+                const auto [snp, cnt] = segs[g];
+                if (cnt == 0) continue;
+                const bool cap = nw && g + 1 == segs.size();
+                plan.push_back({snp, row0, cnt, add_tables(snp, row0, cnt), 0, cap});
+                row0 += cnt * 2 * snp;
+            }
             for (size_t l = 0; l < plan.size(); l++) {
                 if (l > 0) plan[l].flags |= kPairCarryIn;
                 if (l + 1 == plan.size()) plan[l].flags |= kPairFinal;

@@ -458,7 +458,7 @@ strip_f16m_kernel(const StripArgs a) {
 // inside the last block.
 // ---------------------------------------------------------------------------
 template <int NP, bool NW, bool CAP>
-__global__ void __launch_bounds__(64 * kPairWaves, 4)
+__global__ void __launch_bounds__(64 * kPairWaves, NP <= 16 ? 4 : 3)
 pair_kernel(const StripArgs a) {
     constexpr int W = kPairWaves;
     constexpr int ROWW = NP + 4;
@@ -872,6 +872,10 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
 
 hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st) {
     if (a.ngroups == 0 || a.nstrips == 0) return hipSuccess;
+    if (np == 24) {
+        if (!nw) return launch_pair_t<24, false, false>(a, lds_bytes, st);
+        return cap ? launch_pair_t<24, true, true>(a, lds_bytes, st) : launch_pair_t<24, true, false>(a, lds_bytes, st);
+    }
     if (np == 8) {
         if (!nw) return launch_pair_t<8, false, false>(a, lds_bytes, st);
         return cap ? launch_pair_t<8, true, true>(a, lds_bytes, st) : launch_pair_t<8, true, false>(a, lds_bytes, st);

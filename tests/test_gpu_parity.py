@@ -114,7 +114,7 @@ def test_random_golden_full_score_vectors(fname):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 48, 49, 63, 64, 65, 100])
+@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 80, 81, 96, 97, 100])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_query_length_edges_vs_oracle(qlen, algo):
     rng = np.random.default_rng(qlen)
@@ -136,9 +136,17 @@ def test_query_length_edges_vs_oracle(qlen, algo):
             S.set_option("sw_kernel", swk)
             for np_ in (8, 16, 32):
                 S.set_option("strip_np", np_)
-                sc, ids = _full_scores(qq, algo, len(keep))
-                assert (ids == keep).all()
-                assert (sc == exp).all(), (swk, np_, np.nonzero(sc != exp)[0][:10])
+                for pnp in ((16, 24) if swk == 0 and np_ == 16 else (24,)):
+                    S.set_option("pair_np", pnp)
+                    sc, ids = _full_scores(qq, algo, len(keep))
+                    assert (ids == keep).all()
+                    assert (sc == exp).all(), (swk, np_, pnp, np.nonzero(sc != exp)[0][:10])
+                    # the sparse (device-filtered) path with the same plan
+                    for k in (1, 10):
+                        fn = S.sw_align if algo == S.SW else S.nw_align
+                        got = [(h["score"], h["id"]) for h in fn(qq, k, 16)]
+                        assert got == po.topk(exp, keep.astype(np.uint64), k)
+        S.set_option("pair_np", 24)
         S.set_option("strip_np", 16)
         S.set_option("sw_kernel", 0)
         S.free_sequence(qq)
