@@ -44,16 +44,14 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
     dfree(d_work); dfree(d_smax);
-    dfree(d_cand); dfree(d_cand_score); dfree(d_summary); dfree(d_thresh); dfree(d_fcount); dfree(d_thresh_local);
-    if (h_cand) (void)hipHostFree(h_cand);
-    if (h_cand_score) (void)hipHostFree(h_cand_score);
-    if (h_fcount) (void)hipHostFree(h_fcount);
+    dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
+    if (h_fbuf) (void)hipHostFree(h_fbuf);
     if (h_up) (void)hipHostFree(h_up);
     h_up = nullptr;
     h_up_cap = 0;
-    d_cand = nullptr; d_cand_score = nullptr; d_summary = nullptr; d_thresh = nullptr; d_fcount = nullptr;
+    d_fbuf = nullptr; d_summary = nullptr; d_before = nullptr; d_thresh = nullptr;
     d_thresh_local = nullptr;
-    h_cand = nullptr; h_cand_score = nullptr; h_fcount = nullptr; h_cand_cap = 0;
+    h_fbuf = nullptr; h_cand_cap = 0;
     if (h_scores) (void)hipHostFree(h_scores);
     if (h_ovf) (void)hipHostFree(h_ovf);
     if (h_wide) (void)hipHostFree(h_wide);
@@ -322,16 +320,13 @@ void upload_pack(HostPack& H, int dev) {
     dalloc((void**)&D.d_smax, H.lane_out.size() * 4, "running max");
     {
         const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
-        dalloc((void**)&D.d_cand, std::max<size_t>(E, 1) * 4, "candidates");
-        dalloc((void**)&D.d_cand_score, std::max<size_t>(E, 1) * 4, "candidate scores");
+        dalloc((void**)&D.d_fbuf, 16 + std::max<size_t>(E, 1) * 8, "filter candidates");
         dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
+        dalloc((void**)&D.d_before, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter scan");
         dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
         dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
-        dalloc((void**)&D.d_fcount, 16, "filter counters");
-        D.h_cand_cap = 1 << 16;
-        check(hipHostMalloc((void**)&D.h_cand, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
-        check(hipHostMalloc((void**)&D.h_cand_score, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
-        check(hipHostMalloc((void**)&D.h_fcount, 16, hipHostMallocDefault), "pinned");
+        D.h_cand_cap = 4096;
+        check(hipHostMalloc((void**)&D.h_fbuf, 16 + D.h_cand_cap * 8, hipHostMallocDefault), "pinned");
     }
     dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
     dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
@@ -796,22 +791,22 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
             f.summary = D.d_summary;
             f.thresh = D.d_thresh;
             f.thresh_local = D.d_thresh_local;
-            f.cand = D.d_cand;
-            f.cand_score = D.d_cand_score;
-            f.counters = D.d_fcount;
-            check(hipMemsetAsync(D.d_fcount, 0, 16, st), "memset");
+            f.before = D.d_before;
+            f.ovf_count = D.d_ovf;
+            f.counters = D.d_fbuf;
+            f.cand = (uint2*)(D.d_fbuf + 4);
+            check(hipMemsetAsync(D.d_fbuf, 0, 16, st), "memset");
             check(launch_filter(f, st), "filter launch");
-            check(hipMemcpyAsync(D.h_fcount, D.d_fcount, 16, hipMemcpyDeviceToHost, st), "D2H counters");
-            // optimistic copy of the first candidates (usually all of them)
+            // one copy: counters (incl. the overflow count) + the first candidates
             const size_t first = std::min(D.h_cand_cap, E);
-            check(hipMemcpyAsync(D.h_cand, D.d_cand, 4 * first, hipMemcpyDeviceToHost, st), "D2H cand");
-            check(hipMemcpyAsync(D.h_cand_score, D.d_cand_score, 4 * first, hipMemcpyDeviceToHost, st),
-                  "D2H cand scores");
+            check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, 16 + 8 * first, hipMemcpyDeviceToHost, st), "D2H candidates");
         } else {
             check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
         }
-        check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
-        check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
+        if (!out.sparse) {
+            check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
+            check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
+        }
         check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
         if (trace_on()) {
@@ -834,26 +829,34 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
             check(hipEventElapsedTime(&u, D.ev[4], D.ev[0]), "elapsed");
             upload += u;
         }
+        uint32_t nov;
         if (out.sparse) {
-            const uint32_t nc = D.h_fcount[0];
+            const uint32_t nc = D.h_fbuf[0];
+            nov = D.h_fbuf[3];
+            const uint2* cand = (const uint2*)(D.h_fbuf + 4);
+            std::vector<uint2> more;
             if (nc > D.h_cand_cap) {
-                (void)hipHostFree(D.h_cand);
-                (void)hipHostFree(D.h_cand_score);
-                D.h_cand_cap = std::max<size_t>(nc, 2 * D.h_cand_cap);
-                check(hipHostMalloc((void**)&D.h_cand, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
-                check(hipHostMalloc((void**)&D.h_cand_score, D.h_cand_cap * 4, hipHostMallocDefault), "pinned");
-                check(hipMemcpy(D.h_cand, D.d_cand, 4 * (size_t)nc, hipMemcpyDeviceToHost), "D2H cand");
-                check(hipMemcpy(D.h_cand_score, D.d_cand_score, 4 * (size_t)nc, hipMemcpyDeviceToHost), "D2H cand");
+                more.resize(nc);
+                check(hipMemcpy(more.data(), D.d_fbuf + 4, 8 * (size_t)nc, hipMemcpyDeviceToHost), "D2H candidates");
+                cand = more.data();
             }
-            out.cand.assign(D.h_cand, D.h_cand + nc);
-            for (uint32_t i = 0; i < nc; i++) hs[D.h_cand[i]] = D.h_cand_score[i];
+            out.cand.resize(nc);
+            for (uint32_t i = 0; i < nc; i++) {
+                out.cand[i] = cand[i].x;
+                hs[cand[i].x] = (int32_t)cand[i].y;
+            }
             std::sort(out.cand.begin(), out.cand.end());
-            out.dev_o8 += D.h_fcount[1];
-            out.dev_o16 += D.h_fcount[2];
+            out.dev_o8 += D.h_fbuf[1];
+            out.dev_o16 += D.h_fbuf[2];
+            if (nov > 0 && nov <= kOvfCap) {
+                check(hipMemcpy(D.h_ovf, D.d_ovf, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
+                check(hipMemcpy(D.h_wide, D.d_wide, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
+            }
+        } else {
+            nov = D.h_ovf[0];
         }
-        uint32_t nov = D.h_ovf[0];
         if (nov > kOvfCap) fatal("overflow list exhausted (%u entries)", nov);
-        if (nov > 4096) {
+        if (!out.sparse && nov > 4096) {
             check(hipMemcpy(D.h_ovf, D.d_ovf, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
             check(hipMemcpy(D.h_wide, D.d_wide, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
         }

@@ -39,15 +39,12 @@ struct DeviceDB {
     uint32_t* d_lane_out = nullptr;
     uint32_t* d_smax = nullptr;           // SW running max between pair_kernel launches
     // top-k candidate filter (kernels.h FilterArgs)
-    uint32_t* d_cand = nullptr;
-    int32_t* d_cand_score = nullptr;
+    uint32_t* d_fbuf = nullptr;           // [4] counters, then (index, score) x entries
     int32_t* d_summary = nullptr;
+    int32_t* d_before = nullptr;
     int32_t* d_thresh = nullptr;
     int32_t* d_thresh_local = nullptr;
-    uint32_t* d_fcount = nullptr;
-    uint32_t* h_cand = nullptr;           // pinned, h_cand_cap entries
-    int32_t* h_cand_score = nullptr;
-    uint32_t* h_fcount = nullptr;
+    uint32_t* h_fbuf = nullptr;           // pinned: counters + h_cand_cap candidates
     size_t h_cand_cap = 0;
     uint8_t* h_up = nullptr;              // pinned staging for per-search uploads
     size_t h_up_cap = 0;

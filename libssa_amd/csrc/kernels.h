@@ -71,9 +71,10 @@ struct FilterArgs {
     int32_t* summary;          // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
     int32_t* thresh;           // [nblocks] bound from earlier blocks
     int32_t* thresh_local;     // [nblocks * 64] bound from earlier minis of the same block
-    uint32_t* cand;            // [n] candidate entry indices (unordered)
-    int32_t* cand_score;       // [n] their scores
-    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows
+    int32_t* before;           // [nblocks][kFilterMaxK] scan scratch
+    const uint32_t* ovf_count; // copied into counters[3] (one host copy fetches everything)
+    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows, [3] overflowed lanes
+    uint2* cand;               // [n] (entry index, score) of the candidates, unordered; follows counters
 };
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 

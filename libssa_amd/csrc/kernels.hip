@@ -790,44 +790,75 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
     }
 }
 
-// One wave: running top-k over the block summaries (descending, one per
-// lane).  Merge = bitonic: max(run[i], blk[63-i]) holds the 64 largest of
-// the union as a bitonic sequence, six compare-exchange stages sort it.
-__global__ void __launch_bounds__(64) filter_prefix(const FilterArgs a) {
-    const int lane = threadIdx.x;
+// Top-k of two descending lists (one element per lane, lanes >= K hold
+// INT32_MIN): max(a[i], b[63-i]) holds the 64 largest of the union as a
+// bitonic sequence; six compare-exchange stages sort it.
+__device__ __forceinline__ int32_t merge_topk(int32_t x, int32_t y, int lane, int K) {
+    int32_t v = max(x, __shfl(y, 63 - lane));
+    for (int j = 32; j > 0; j >>= 1) {
+        const int32_t o = __shfl_xor(v, j);
+        v = (lane & j) ? min(v, o) : max(v, o);
+    }
+    return lane < K ? v : INT32_MIN;
+}
+
+// Exclusive prefix of the block summaries under top-k merge, as a blocked
+// scan: each of 16 waves scans its run of blocks (keeping the state before
+// every block), wave 0 scans the 16 run totals, and every wave merges its
+// carry-in into the stored states.  T[b] = k-th largest of all mini maxima
+// of blocks < b.
+constexpr int kPrefixWaves = 16;
+__global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterArgs a) {
+    __shared__ int32_t carry[kPrefixWaves][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = (int)a.k;
+    const uint32_t per = (a.nblocks + kPrefixWaves - 1) / kPrefixWaves;
+    const uint32_t b0 = min(a.nblocks, wave * per), b1 = min(a.nblocks, b0 + per);
     int32_t run = INT32_MIN;
-    int32_t nxt = a.nblocks ? a.summary[lane] : INT32_MIN;
-    for (uint32_t b = 0; b < a.nblocks; b++) {
+    int32_t nxt = b0 < b1 ? a.summary[(size_t)b0 * kFilterMaxK + lane] : INT32_MIN;
+    for (uint32_t b = b0; b < b1; b++) {
         const int32_t blk = nxt;
-        if (b + 1 < a.nblocks) nxt = a.summary[(size_t)(b + 1) * kFilterMaxK + lane];
-        const int32_t t = __builtin_amdgcn_readlane(run, K - 1);
-        if (lane == 0) a.thresh[b] = t;
-        int32_t v = max(run, __shfl(blk, 63 - lane));
-        for (int j = 32; j > 0; j >>= 1) {
-            const int32_t o = __shfl_xor(v, j);
-            v = (lane & j) ? min(v, o) : max(v, o);
+        if (b + 1 < b1) nxt = a.summary[(size_t)(b + 1) * kFilterMaxK + lane];
+        a.before[(size_t)b * kFilterMaxK + lane] = run;
+        run = merge_topk(run, blk, lane, K);
+    }
+    carry[wave][lane] = run;
+    __syncthreads();
+    if (wave == 0) {
+        int32_t c = INT32_MIN;
+        for (int w = 0; w < kPrefixWaves; w++) {
+            const int32_t t = carry[w][lane];
+            carry[w][lane] = c;
+            c = merge_topk(c, t, lane, K);
         }
-        run = lane < K ? v : INT32_MIN;
+    }
+    __syncthreads();
+    const int32_t c = carry[wave][lane];
+    nxt = b0 < b1 ? a.before[(size_t)b0 * kFilterMaxK + lane] : INT32_MIN;
+    for (uint32_t b = b0; b < b1; b++) {
+        const int32_t st = nxt;
+        if (b + 1 < b1) nxt = a.before[(size_t)(b + 1) * kFilterMaxK + lane];
+        const int32_t t = __builtin_amdgcn_readlane(merge_topk(c, st, lane, K), K - 1);
+        if (lane == 0) a.thresh[b] = t;
     }
 }
 
 __global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e == 0) a.counters[3] = *a.ovf_count;
     if (e >= a.n) return;
     const int32_t x = a.scores[e];
     const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
     if (x == INT32_MIN || x > t) {
         const uint32_t i = atomicAdd(&a.counters[0], 1u);
-        a.cand[i] = e;
-        a.cand_score[i] = x;
+        a.cand[i] = make_uint2(e, (uint32_t)x);
     }
 }
 
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
     hipLaunchKernelGGL(filter_block, dim3(a.nblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(filter_prefix, dim3(1), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(filter_prefix, dim3(1), dim3(64 * kPrefixWaves), 0, st, a);
     hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
     return hipGetLastError();
 }
