@@ -65,6 +65,12 @@ typedef struct {
 int ssa_amd_device_count( void );
 void ssa_amd_set_device( int device );
 void ssa_amd_set_id_offset( size_t offset );
+/* Search on several devices from this one process (one host thread per
+ * device inside sw_align / nw_align, the DB split into contiguous record
+ * ranges at chunk_size boundaries, balanced by residues; results identical
+ * to a single device).  n = 0 returns to single-device mode
+ * (ssa_amd_set_device).  Returns 0, or 1 for an invalid device list. */
+int ssa_amd_set_devices( const int * devices, int n );
 int ssa_amd_prepare_db( void );            /* pack + upload the DB now; returns 0 on success */
 void ssa_amd_get_stats( ssa_amd_stats_t * out );
 void ssa_amd_set_option( const char * name, long value );

@@ -80,7 +80,7 @@ EXPORTS = {
                       "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
                       "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
                       "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
-                      "ssa_amd_save_db", "ssa_amd_load_db"],
+                      "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -115,6 +115,7 @@ def load():
         "ssa_amd_replay": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
         "ssa_amd_query_views": ([P, POINTER(q_seq_t), c_size_t], c_size_t),
         "ssa_amd_save_db": ([c_char_p], c_int), "ssa_amd_load_db": ([c_char_p], c_int),
+        "ssa_amd_set_devices": ([POINTER(c_int), c_int], c_int),
         "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
                                c_size_t),
         "ssa_amd_translate": ([c_int, c_char_p, c_size_t, c_int, c_int, c_char_p, c_size_t], c_size_t),
@@ -185,6 +186,12 @@ def device_count():
 
 
 def set_device(dev): load().ssa_amd_set_device(dev)
+
+
+def set_devices(devs):
+    """ssa_amd_set_devices: search on all of `devs` from this process ([] = single device)."""
+    arr = (c_int * max(len(devs), 1))(*devs)
+    return load().ssa_amd_set_devices(arr, len(devs))
 def set_id_offset(off): load().ssa_amd_set_id_offset(off)
 def prepare_db(): return load().ssa_amd_prepare_db()
 def set_option(name, value): load().ssa_amd_set_option(_b(name), value)

@@ -1,9 +1,12 @@
 // api.cpp -- the exported C ABI: every function of include/libssa.h (the
 // reference's src/libssa.h:122-263, implemented in src/libssa.c) plus the
 // MI355X extensions of include/libssa_amd.h.
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "engine.h"
 
@@ -113,41 +116,92 @@ struct SearchResult {
     std::vector<Hit> hits;      // sorted top-k, or the insertion log
 };
 
+void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPlan>& plan) {
+    ssa_amd_stats_t& S = stats();
+    S.kernel_ms = S.wide_ms = S.d2h_ms = S.prep_ms = S.upload_ms = S.sync_wait_ms = 0;
+    S.cells = S.entries = S.wide_count = S.kernel_bytes = 0;
+    for (size_t i = 0; i < sc.size(); i++) {
+        // devices run concurrently: times are the slowest device's
+        S.kernel_ms = std::max(S.kernel_ms, sc[i].kernel_ms);
+        S.wide_ms = std::max(S.wide_ms, sc[i].wide_ms);
+        S.d2h_ms = std::max(S.d2h_ms, sc[i].d2h_ms);
+        S.prep_ms = std::max(S.prep_ms, sc[i].prep_ms);
+        S.upload_ms = std::max(S.upload_ms, sc[i].upload_ms);
+        S.sync_wait_ms = std::max(S.sync_wait_ms, sc[i].sync_wait_ms);
+        S.cells += sc[i].cells;
+        S.entries += sc[i].entries;
+        S.wide_count += sc[i].wide_count;
+        S.kernel_bytes += sc[i].kernel_bytes;
+    }
+    S.kernel_launches = (uint32_t)(sc.empty() ? 0 : sc[0].views);
+    S.device = plan.empty() ? -1 : plan[0].device;
+    snprintf(S.kernel, sizeof S.kernel, "%s", sc.empty() ? "" : sc[0].kernel);
+}
+
 void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {
     const double t0 = now_ms();
     check_width(bw);
     ensure_device_db();
-    const double ta = now_ms();
+    const std::vector<SlotPlan> plan = device_plan();
     R.views = query_views(q);
-    SearchScores sc;
-    const double tb = now_ms();
-    device_search(R.views, algo, k, bw, sc);
+    std::vector<SearchScores> sc(plan.size());
+    std::vector<std::vector<Hit>> logs(plan.size());
+    if (plan.size() == 1) {
+        device_search(device_db(0), R.views, algo, k, bw, sc[0]);
+    } else {
+        // one host thread per device; each replays its shard into a log of
+        // the elements its own heap accepts
+        std::vector<std::thread> pool;
+        for (size_t s = 0; s < plan.size(); s++)
+            pool.emplace_back([&, s]() {
+                check(hipSetDevice(plan[s].device), "hipSetDevice");
+                device_search(device_db(s), R.views, algo, k, bw, sc[s]);
+                TopK h(k);
+                replay(sc[s], device_db(s).meta, R.views, h, &logs[s]);
+            });
+        for (auto& t : pool) t.join();
+    }
     const double t1 = now_ms();
-    if (trace_on())
-        fprintf(stderr, "trace: ensure %.3f views %.3f device_search %.3f\n", ta - t0, tb - ta, t1 - tb);
     TopK heap(k);
-    replay(sc, device_db().meta, R.views, heap, want_log ? &R.hits : nullptr);
+    if (plan.size() == 1) {
+        replay(sc[0], device_db(0).meta, R.views, heap, want_log ? &R.hits : nullptr);
+    } else {
+        for (const auto& L : logs)
+            for (const Hit& h : L)
+                if (heap.add(h) && want_log) R.hits.push_back(h);
+    }
     if (!want_log) R.hits = heap.sorted();
     const double t2 = now_ms();
     uint64_t o8 = 0, o16 = 0;
-    if (bw == BIT_WIDTH_8 || cfg().output_mode >= OUTPUT_INFO) overflow_counters(sc, algo, bw, o8, o16);
-    else if (bw == BIT_WIDTH_16 && algo == kAlgoSW) o16 = sc.wide.size();
+    for (const SearchScores& x : sc) {
+        uint64_t a8 = 0, a16 = 0;
+        if (bw == BIT_WIDTH_8 || cfg().output_mode >= OUTPUT_INFO) overflow_counters(x, algo, bw, a8, a16);
+        else if (bw == BIT_WIDTH_16 && algo == kAlgoSW) a16 = x.wide.size();
+        o8 += a8;
+        o16 += a16;
+    }
+    publish_stats(sc, plan);
     ssa_amd_stats_t& S = stats();
     S.overflow_8 = o8;
     S.overflow_16 = o16;
     S.replay_ms = t2 - t1;
     S.search_ms = now_ms() - t0;
     // m_run's bookkeeping messages (manager.c:147-170)
-    const EntryMeta& M = device_db().meta;
     const size_t cs = cfg().chunk_size;
-    print_info("Device %d - Processed chunks: %ld and sequences: %ld\n", device_db().device,
-               (long)((M.records + cs - 1) / cs), (long)M.size());
+    size_t records = 0, entries = 0;
+    for (size_t s = 0; s < plan.size(); s++) {
+        const EntryMeta& M = device_db(s).meta;
+        print_info("Device %d - Processed chunks: %ld and sequences: %ld\n", device_db(s).device,
+                   (long)((M.records + cs - 1) / cs), (long)M.size());
+        records += M.records;
+        entries += M.size();
+    }
     if (o8 || o16)
         print_info("Overflow occurred: %ld sequences were re-aligned with 16 bit, and %ld sequences with 64 bit\n",
                    (long)o8, (long)o16);
-    if (M.records != M.size())
-        print_warning("# Number of processed sequences differs! Expected: %ld - Actual: %ld\n", (long)M.records,
-                      (long)M.size());
+    if (records != entries)
+        print_warning("# Number of processed sequences differs! Expected: %ld - Actual: %ld\n", (long)records,
+                      (long)entries);
 }
 
 // create_score_alignment_list (aligner.c:62-99): one alignment_t per hit,
@@ -289,7 +343,30 @@ int ssa_amd_device_count(void) {
     return n;
 }
 
-void ssa_amd_set_device(int device) { cfg().device = device; }
+void ssa_amd_set_device(int device) {
+    cfg().device = device;
+    cfg().devices.clear();
+}
+
+int ssa_amd_set_devices(const int* devices, int n) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    if (n <= 0 || !devices) {
+        cfg().devices.clear();
+        return 0;
+    }
+    if ((size_t)n > kMaxSlots) {
+        print_error("At most %d devices per process", (int)kMaxSlots);
+        return 1;
+    }
+    for (int i = 0; i < n; i++)
+        if (devices[i] < 0 || devices[i] >= count) {
+            print_error("No HIP device %d (%d visible)", devices[i], count);
+            return 1;
+        }
+    cfg().devices.assign(devices, devices + n);
+    return 0;
+}
 void ssa_amd_set_id_offset(size_t offset) { cfg().id_offset = offset; }
 
 int ssa_amd_prepare_db(void) {

@@ -15,6 +15,7 @@ namespace ssa {
 constexpr int kDim = 32;          // score matrix is 32 x 32, M(x,y) = m[(x << 5) + y]
 constexpr int kAlgoSW = 0;
 constexpr int kAlgoNW = 1;
+constexpr size_t kMaxSlots = 16;   // devices one process can search on
 
 // ------------------------------------------------------------------ config
 struct Config {
@@ -26,6 +27,7 @@ struct Config {
     int q_gencode = 1, d_gencode = 1;
     int8_t gap_open = 0, gap_extend = 0;  // libssa.c:35-36
     int device = -1;                      // -1: current HIP device
+    std::vector<int> devices;             // ssa_amd_set_devices: shard the DB over these
     size_t id_offset = 0;                 // global ID of local record 0
     uint64_t db_generation = 0;           // bumped by init_db
     // tuning knobs (ssa_amd_set_option)

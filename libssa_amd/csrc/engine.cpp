@@ -30,9 +30,10 @@ void check(hipError_t e, const char* what) {
     if (e != hipSuccess) fatal("HIP error in %s: %s", what, hipGetErrorString(e));
 }
 
-DeviceDB& device_db() {
-    static DeviceDB d;
-    return d;
+DeviceDB& device_db(size_t slot) {
+    static DeviceDB slots[kMaxSlots];
+    if (slot >= kMaxSlots) fatal("device slot %zu out of range", slot);
+    return slots[slot];
 }
 
 static void dfree(void* p) {
@@ -170,13 +171,13 @@ unsigned host_threads() { return std::max(1u, std::min(16u, std::thread::hardwar
 
 // The plugin is called from several threads at once, as the reference's
 // own search threads do (adp_next_chunk runs in every worker).
-void stage_from_plugin(Staged& S) {
-    const size_t count = ssa_db_get_sequence_count();
+void stage_from_plugin(Staged& S, size_t rb, size_t re) {
+    const size_t count = re - rb;
     const unsigned nth = count < 20000 ? 1u : host_threads();
     std::vector<Staged> part(nth);
     std::vector<std::thread> pool;
     for (unsigned t = 0; t < nth; t++)
-        pool.emplace_back([&, t]() { stage_range(count * t / nth, count * (t + 1) / nth, part[t]); });
+        pool.emplace_back([&, t]() { stage_range(rb + count * t / nth, rb + count * (t + 1) / nth, part[t]); });
     for (auto& th : pool) th.join();
     S.meta.records = count;
     size_t ne = 0, nc = 0;
@@ -211,9 +212,9 @@ struct HostPack {
     uint64_t blocks = 0;
 };
 
-void build_host_pack(HostPack& H) {
+void build_host_pack(HostPack& H, size_t rb, size_t re) {
     Staged S;
-    stage_from_plugin(S);
+    stage_from_plugin(S, rb, re);
     const size_t E = S.meta.size();
 
     // length-sorted groups of 64 lanes (longest first: long waves start
@@ -298,8 +299,7 @@ void build_host_pack(HostPack& H) {
     H.meta = std::move(S.meta);
 }
 
-void upload_pack(HostPack& H, int dev) {
-    DeviceDB& D = device_db();
+void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     const Config& C = cfg();
     D.release();
     check(hipSetDevice(dev), "hipSetDevice");
@@ -352,12 +352,6 @@ void upload_pack(HostPack& H, int dev) {
     D.dgencode = C.d_gencode;
 }
 
-int current_device() {
-    int dev = cfg().device;
-    if (dev < 0) check(hipGetDevice(&dev), "hipGetDevice");
-    return dev;
-}
-
 // ------------------------------------------------------ packed DB files
 // "SSAPACK1" | u32 version, symtype, strands, dgencode | u64 records,
 // entries, residues, ngroups, blocks | u32 alpha, 0 | u8 code_of[32] |
@@ -373,24 +367,87 @@ bool rd(FILE* f, T* p, size_t n) { return n == 0 || fread(p, sizeof(T), n, f) ==
 
 }  // namespace
 
-void ensure_device_db() {
-    DeviceDB& D = device_db();
+std::vector<SlotPlan> device_plan() {
     const Config& C = cfg();
-    const int dev = current_device();
-    if (D.generation == C.db_generation && D.device == dev && D.symtype == C.symtype &&
-        D.strands == C.strands && D.dgencode == C.d_gencode)
-        return;
-    const double t0 = now_ms();
-    check(hipSetDevice(dev), "hipSetDevice");
+    const size_t count = ssa_db_get_sequence_count();
+    if (C.devices.size() <= 1) {
+        int dev = C.devices.empty() ? C.device : C.devices[0];
+        if (dev < 0) check(hipGetDevice(&dev), "hipGetDevice");
+        return {{dev, 0, count}};
+    }
+    // cut at chunk boundaries, balancing residues (cached per DB generation)
+    static uint64_t gen = ~0ull;
+    static std::vector<int> devs;
+    static size_t chunk = 0, cnt = 0;
+    static std::vector<SlotPlan> plan;
+    if (gen == C.db_generation && devs == C.devices && chunk == C.chunk_size && cnt == count) return plan;
+    const size_t cs = C.chunk_size, nchunks = (count + cs - 1) / cs, n = C.devices.size();
+    std::vector<uint64_t> cum(nchunks + 1, 0);
+    for (size_t c = 0; c < nchunks; c++) {
+        uint64_t r = 0;
+        for (size_t i = c * cs; i < std::min(count, (c + 1) * cs); i++) {
+            p_seqinfo si = ssa_db_get_sequence(i);
+            if (si) r += si->seqlen;
+        }
+        cum[c + 1] = cum[c] + r;
+    }
+    plan.clear();
+    size_t c0 = 0;
+    for (size_t s = 0; s < n; s++) {
+        size_t c1 = nchunks;
+        if (s + 1 < n) {
+            const uint64_t target = cum[nchunks] * (s + 1) / n;
+            c1 = (size_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+            c1 = std::max(c0, std::min(c1, nchunks));
+        }
+        plan.push_back({C.devices[s], std::min(count, c0 * cs), std::min(count, c1 * cs)});
+        c0 = c1;
+    }
+    gen = C.db_generation;
+    devs = C.devices;
+    chunk = C.chunk_size;
+    cnt = count;
+    return plan;
+}
+
+bool ensure_device_db(size_t slot, const SlotPlan& p) {
+    DeviceDB& D = device_db(slot);
+    const Config& C = cfg();
+    if (D.generation == C.db_generation && D.device == p.device && D.symtype == C.symtype &&
+        D.strands == C.strands && D.dgencode == C.d_gencode && D.rec_begin == p.rec_begin && D.rec_end == p.rec_end)
+        return false;
+    check(hipSetDevice(p.device), "hipSetDevice");
     HostPack H;
-    build_host_pack(H);
-    upload_pack(H, dev);
-    stats().pack_ms = now_ms() - t0;
+    build_host_pack(H, p.rec_begin, p.rec_end);
+    upload_pack(D, H, p.device);
+    D.rec_begin = p.rec_begin;
+    D.rec_end = p.rec_end;
+    return true;
+}
+
+void ensure_device_db() {
+    const std::vector<SlotPlan> plan = device_plan();
+    const double t0 = now_ms();
+    bool packed = false;
+    if (plan.size() == 1) {
+        packed = ensure_device_db(0, plan[0]);
+    } else {
+        std::vector<char> did(plan.size(), 0);
+        std::vector<std::thread> pool;
+        for (size_t s = 0; s < plan.size(); s++) pool.emplace_back([&, s]() { did[s] = ensure_device_db(s, plan[s]); });
+        for (auto& t : pool) t.join();
+        for (char d : did) packed |= d != 0;
+    }
+    if (packed) stats().pack_ms = now_ms() - t0;
 }
 
 int save_packed_db(const char* path) {
+    if (device_plan().size() != 1) {
+        print_error("Packed DB files are written from a single-device DB");
+        return 1;
+    }
     ensure_device_db();
-    DeviceDB& D = device_db();
+    DeviceDB& D = device_db(0);
     FILE* f = fopen(path, "wb");
     if (!f) {
         print_error("Cannot open packed DB file for writing: %s", path);
@@ -443,6 +500,8 @@ int load_packed_db(const char* path) {
     if ((int)hdr32[1] != C.symtype || (int)hdr32[2] != C.strands || (int)hdr32[3] != C.d_gencode)
         return fail("packed for another symbol type / strands / genetic code");
     if (hdr64[0] != ssa_db_get_sequence_count()) return fail("record count differs from the open DB");
+    const std::vector<SlotPlan> plan = device_plan();
+    if (plan.size() != 1) return fail("packed DB files load into a single device");
     const uint64_t E = hdr64[1], ng = hdr64[3];
     if (alpha[0] > 31 || E > ng * 64 || ng > E / 64 + 1) return fail("corrupt header");
     H.meta.records = hdr64[0];
@@ -471,7 +530,10 @@ int load_packed_db(const char* path) {
         }
     }
     const double t0 = now_ms();
-    upload_pack(H, current_device());
+    DeviceDB& D = device_db(0);
+    upload_pack(D, H, plan[0].device);
+    D.rec_begin = 0;
+    D.rec_end = hdr64[0];
     stats().pack_ms = now_ms() - t0;
     return 0;
 }
@@ -526,8 +588,7 @@ static uint32_t nw_f16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM,
     return (uint32_t)a;
 }
 
-void device_search(const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out) {
-    DeviceDB& D = device_db();
+void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out) {
     check(hipSetDevice(D.device), "hipSetDevice");
     const Config& C = cfg();
     const size_t E = D.meta.size();
@@ -878,20 +939,15 @@ void device_search(const std::vector<QueryView>& views, int algo, size_t k, int 
     }
     if (trace_on())
         fprintf(stderr, "trace: prep %.3f sync %.3f total %.3f\n", prep, sync_wait, now_ms() - t_prep0);
-    ssa_amd_stats_t& S = stats();
-    S.kernel_ms = kms;
-    S.prep_ms = V == 1 ? prep : 0;
-    S.upload_ms = upload;
-    S.sync_wait_ms = sync_wait;
-    S.wide_ms = wms;
-    S.d2h_ms = dms;
-    S.cells = out.cells;
-    S.entries = E;
-    S.wide_count = wide_total;
-    S.kernel_launches = (uint32_t)V;
-    S.device = D.device;
-    S.kernel_bytes = kernel_bytes;
-    snprintf(S.kernel, sizeof S.kernel, "%s", kname);
+    out.kernel_ms = kms;
+    out.prep_ms = V == 1 ? prep : 0;
+    out.upload_ms = upload;
+    out.sync_wait_ms = sync_wait;
+    out.wide_ms = wms;
+    out.d2h_ms = dms;
+    out.wide_count = wide_total;
+    out.kernel_bytes = kernel_bytes;
+    out.kernel = kname;
 }
 
 }  // namespace ssa

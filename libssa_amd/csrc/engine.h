@@ -68,11 +68,24 @@ struct DeviceDB {
     // for residue code code_of[c]; code alpha is the padding column
     std::vector<uint8_t> code_of;
     uint32_t alpha = 0;
+    size_t rec_begin = 0, rec_end = 0;    // plugin records [rec_begin, rec_end) of this shard
     void release();
 };
-DeviceDB& device_db();
-void ensure_device_db();                  // (re)packs from the plugin when stale
-int save_packed_db(const char* path);     // 0 on success
+
+// One slot per device the library searches on: slot 0 alone (the current
+// HIP device or ssa_amd_set_device) by default; with ssa_amd_set_devices the
+// DB is split into contiguous record ranges, one per device, cut at
+// chunk_size boundaries (so the reference's insertion order is the
+// concatenation of the slots' orders) and balanced by residues.
+struct SlotPlan {
+    int device;
+    size_t rec_begin, rec_end;
+};
+std::vector<SlotPlan> device_plan();
+DeviceDB& device_db(size_t slot = 0);
+bool ensure_device_db(size_t slot, const SlotPlan& p);   // (re)packs from the plugin when stale
+void ensure_device_db();                  // every slot of device_plan()
+int save_packed_db(const char* path);     // 0 on success (single device)
 int load_packed_db(const char* path);     // 0 on success; replaces packing from the plugin
 std::vector<uint8_t> fetch_entry_codes(uint64_t local_id, int strand, int frame);
 
@@ -90,6 +103,10 @@ struct SearchScores {
     uint64_t dev_o8 = 0, dev_o16 = 0;
     std::unordered_map<uint64_t, int64_t> wide;   // key = view * entries + entry
     uint64_t cells = 0;
+    // device-side timing and counts of this search (published to stats())
+    double kernel_ms = 0, wide_ms = 0, d2h_ms = 0, prep_ms = 0, upload_ms = 0, sync_wait_ms = 0;
+    uint64_t wide_count = 0, kernel_bytes = 0;
+    const char* kernel = "";
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;
@@ -98,7 +115,7 @@ struct SearchScores {
     }
 };
 // k / bit_width decide whether the device top-k filter applies
-void device_search(const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out);
+void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out);
 
 ssa_amd_stats_t& stats();
 void check(hipError_t e, const char* what);

@@ -569,3 +569,39 @@ def test_packed_db_save_load_roundtrip(tmp_path):
     S.free_sequence(qn)
     del seqs
     S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+
+
+@pytest.mark.parametrize("nslots", [2, 3])
+def test_multi_device_slots_match_single_device(nslots):
+    """ssa_amd_set_devices: the DB split over several device slots (here all
+    on the one GPU of the box, which exercises the same split, per-slot
+    packing, threads and log merge) returns exactly the single-device
+    results -- protein (one view) and NUCLEOTIDE both strands (two views,
+    chunk-interleaved insertion order)."""
+    q = syn.protein_query(90, 12)
+    codes, off = syn.protein_db(6000, 13, query=q, plant_every=700, lo=1, hi=500)
+    with tempfile.TemporaryDirectory() as tmp:
+        configure(False, ("builtin", "blosum62"), -11, -1, chunk=97)
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        runs = []
+        for devs in ([], [0] * nslots):
+            assert S.set_devices(devs) == 0
+            runs.append([[(h["score"], h["id"]) for h in fn(qq, k, 16)]
+                         for fn in (S.sw_align, S.nw_align) for k in (1, 10, 64, 500)]
+                        + [S.search(qq, S.SW, 25, 16, S.LOG)])
+        assert runs[0] == runs[1]
+        S.free_sequence(qq)
+        configure(True, ("const", 2, -3), -5, -2, chunk=37, strands=S.BOTH_STRANDS)
+        S.init_db(os.path.join(DATA, "AF091148.fas"))
+        qn = S.init_sequence_fasta(S.READ_FROM_FILE, os.path.join(DATA, "one_seq.fas"))
+        runs = []
+        for devs in ([], [0] * nslots):
+            assert S.set_devices(devs) == 0
+            runs.append([[(h["score"], h["id"], h["db_strand"]) for h in fn(qn, k, 16)]
+                         for fn in (S.sw_align, S.nw_align) for k in (3, 50)])
+        assert runs[0] == runs[1]
+        S.free_sequence(qn)
+    S.set_devices([])
+    S.set_chunk_size(1000)
+    S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
