@@ -605,3 +605,45 @@ def test_multi_device_slots_match_single_device(nslots):
     S.set_devices([])
     S.set_chunk_size(1000)
     S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_full_size_config_properties(cfg, tmp_path):
+    """BASELINE.json sizes (1 M sequences; C2 SW q=400 BLOSUM62 -11/-1, C3 NW
+    q=1000 BLOSUM50 -10/-2), checked through size-independent properties:
+    the default f16 pair kernel and the independent int16 strip kernel agree
+    on all 1 M scores; the oracle's int64 scores agree on a seeded sample of
+    500 entries and on every top-100 hit; the top-k lists from the device
+    filter equal a host replay of the full score vector."""
+    algo, mname, go, ge, qlen = (S.SW, "blosum62", -11, -1, 400) if cfg == "c2" else (S.NW, "blosum50", -10, -2, 1000)
+    q = syn.protein_query(qlen, 7)
+    codes, off = syn.protein_db(1_000_000, 42, query=q, plant_every=10000, sampler="lut")
+    configure(False, ("builtin", mname), go, ge)
+    path = str(tmp_path / "big.fas")
+    syn.write_fasta(path, codes, off)
+    S.init_db(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    n = len(off) - 1
+    vecs = {}
+    for swk in (0, 1):
+        S.set_option("sw_kernel", swk)
+        log = S.search(qq, algo, n + 1, 16, S.LOG, cap=n + 8)
+        assert len(log) == n
+        vecs[swk] = np.array([h[0] for h in log], np.int64)
+        assert S.stats()["kernel"] == (("pair_f16_" if swk == 0 else "strip16_") + ("sw" if algo == S.SW else "nw"))
+    S.set_option("sw_kernel", 0)
+    assert (vecs[0] == vecs[1]).all(), np.nonzero(vecs[0] != vecs[1])[0][:10]
+    sc = vecs[0]
+    M = TABLES["matrices"][NAMES.index(mname)].copy()
+    rng = np.random.default_rng(99)
+    top = np.argsort(-sc, kind="stable")[:100]
+    sample = np.unique(np.concatenate([rng.choice(n, 500, replace=False), top]))
+    seqs = [codes[int(off[i]):int(off[i + 1])] for i in sample]
+    db, soff = po.pack_db(seqs)
+    exp = po.scores(algo, q, db, soff, M, go, ge)
+    assert (exp == sc[sample]).all()
+    ids = np.arange(n, dtype=np.uint64)
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    for k in (1, 10, 64):
+        assert [(h["score"], h["id"]) for h in fn(qq, k, 16)] == po.topk(sc, ids, k)
+    S.free_sequence(qq)
