@@ -60,7 +60,8 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--strip-np", type=int, default=16)
+    p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
+    p.add_argument("--pair-np", type=int, default=24, help="pair kernel main strip: 24 (48 rows) or 16 (32 rows)")
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
     args = p.parse_args()
     cfg = CONFIGS[args.config]
@@ -149,6 +150,7 @@ def main():
     S.set_device(local)
     S.set_output_mode(S.OUTPUT_ERROR)
     S.set_option("strip_np", args.strip_np)
+    S.set_option("pair_np", args.pair_np)
     for o in args.option:
         k, v = o.split("=")
         S.set_option(k, int(v))
@@ -239,14 +241,14 @@ def main():
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
-        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_np{args.strip_np}")
+        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_pair{args.pair_np}")
         if rec:
             traffic = rec["bytes_per_launch"]
     # VALU issue roofline: the strip kernel is made of
     # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
     # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
     # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_c2_sw_np16).
-    instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 else None
+    instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 and args.pair_np == 24 else None
     issue_cycles = 4.17
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
@@ -266,7 +268,7 @@ def main():
                                f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
                                f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
                    "db_seqs_per_gpu": args.seqs, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
-                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "strip_np": args.strip_np,
+                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_np": args.pair_np, "strip_np": args.strip_np,
                    "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
