@@ -81,6 +81,16 @@ void ssa_amd_set_option( const char * name, long value );
 size_t ssa_amd_search( p_query query, int algo, size_t hitcount, int bit_width, int mode,
                        ssa_hit_t * out, size_t cap );
 
+/* Several queries against the open DB in one call.
+ * Query i's sorted top-k goes to out[i * hitcount ...], its length to
+ * counts[i]; returns the total.  Each query is exactly sw_align/nw_align's
+ * result.  The DB is packed once and stays in HBM; per query the library
+ * adds ~0.1 ms of fixed work (profile upload, filter, replay) to the DP,
+ * which is VALU-bound, so there is no DB streaming for a batch to amortise
+ * (DESIGN.md §7). */
+size_t ssa_amd_search_batch( const p_query * queries, size_t nq, int algo, size_t hitcount, int bit_width,
+                             ssa_hit_t * out, size_t * counts );
+
 /* Replays an insertion log (concatenated shard logs, in shard order) and
  * writes the sorted top-k (score desc, id desc).  Returns the count. */
 size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );

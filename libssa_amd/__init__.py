@@ -80,7 +80,7 @@ EXPORTS = {
                       "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
                       "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
                       "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
-                      "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices"],
+                      "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -116,6 +116,8 @@ def load():
         "ssa_amd_query_views": ([P, POINTER(q_seq_t), c_size_t], c_size_t),
         "ssa_amd_save_db": ([c_char_p], c_int), "ssa_amd_load_db": ([c_char_p], c_int),
         "ssa_amd_set_devices": ([POINTER(c_int), c_int], c_int),
+        "ssa_amd_search_batch": ([POINTER(c_void_p), c_size_t, c_int, c_size_t, c_int, POINTER(ssa_hit_t),
+                                  POINTER(c_size_t)], c_size_t),
         "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
                                c_size_t),
         "ssa_amd_translate": ([c_int, c_char_p, c_size_t, c_int, c_int, c_char_p, c_size_t], c_size_t),
@@ -258,3 +260,14 @@ def align_pair(algo, query_codes, db_codes):
     buf = ctypes.create_string_buffer(n + 1)
     L.ssa_amd_align_pair(algo, q, len(q), d, len(d), reg, buf, n + 1)
     return tuple(reg), buf.value.decode()
+
+
+def search_batch(queries, algo, hitcount, bit_width=BIT_WIDTH_16):
+    """ssa_amd_search_batch: per query, the sorted top-k [(score, id), ...]."""
+    L = load()
+    nq = len(queries)
+    qs = (c_void_p * max(nq, 1))(*queries)
+    out = (ssa_hit_t * max(nq * hitcount, 1))()
+    counts = (c_size_t * max(nq, 1))()
+    L.ssa_amd_search_batch(qs, nq, algo, hitcount, bit_width, out, counts)
+    return [[(out[i * hitcount + j].score, out[i * hitcount + j].db_id) for j in range(counts[i])] for i in range(nq)]

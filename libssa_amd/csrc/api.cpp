@@ -444,6 +444,33 @@ size_t ssa_amd_search(p_query query, int algo, size_t hitcount, int bit_width, i
     return n;
 }
 
+size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t hitcount, int bit_width,
+                            ssa_hit_t* out, size_t* counts) {
+    size_t total = 0;
+    const double t0 = now_ms();
+    double kms = 0;
+    uint64_t cells = 0;
+    for (size_t i = 0; i < nq; i++) {
+        test_configuration(queries[i]);
+        SearchResult R;
+        run_search(queries[i], algo == SSA_AMD_NW ? kAlgoNW : kAlgoSW, hitcount, bit_width, false, R);
+        kms += stats().kernel_ms;
+        cells += stats().cells;
+        const size_t n = std::min(hitcount, R.hits.size());
+        for (size_t j = 0; j < n; j++) {
+            const Hit& h = R.hits[j];
+            out[i * hitcount + j] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
+        }
+        if (counts) counts[i] = n;
+        total += n;
+    }
+    ssa_amd_stats_t& S = stats();
+    S.kernel_ms = kms;
+    S.cells = cells;
+    S.search_ms = now_ms() - t0;
+    return total;
+}
+
 size_t ssa_amd_replay(const ssa_hit_t* log, size_t n, size_t hitcount, ssa_hit_t* out) {
     TopK heap(hitcount);
     for (size_t i = 0; i < n; i++) {

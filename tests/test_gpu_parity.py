@@ -647,3 +647,18 @@ def test_full_size_config_properties(cfg, tmp_path):
     for k in (1, 10, 64):
         assert [(h["score"], h["id"]) for h in fn(qq, k, 16)] == po.topk(sc, ids, k)
     S.free_sequence(qq)
+
+
+def test_search_batch_matches_single_queries():
+    """ssa_amd_search_batch returns each query's sw_align/nw_align result."""
+    codes, off = syn.protein_db(3000, 21, lo=1, hi=500)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qs = [S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(syn.protein_query(n, n)))
+              for n in (5, 30, 64, 200, 401)]
+        for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+            for k in (1, 20, 100):
+                assert S.search_batch(qs, algo, k) == [[(h["score"], h["id"]) for h in fn(q, k, 16)] for q in qs]
+        for q in qs:
+            S.free_sequence(q)
