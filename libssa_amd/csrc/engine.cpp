@@ -561,25 +561,29 @@ static uint32_t nw_int16_limit(size_t m, int Q, int R, int64_t minM, int64_t max
     return (uint32_t)a;
 }
 
-// NW on f16 bit patterns (pair_kernel<.., NW=true>): values are stored as
-// v + base and every real value and intermediate of an entry of length n must
-// stay inside [0x0400, 0x7BFF].  Upper bound (m+1)*maxM fixes base; the
-// two-gap lower bound then limits n.  Returns the largest admissible n (0 when
-// the query cannot use the f16 path at all) and the base.
+// NW on f16 bit patterns (pair_kernel<.., NW=true>) works on diagonal-
+// relative values X^ = X - (i+j)R stored as X^ + base; every real value and
+// intermediate of an entry of length n (and of its +1 padding column) must
+// stay inside [0x0400, 0x7BFF].  Lower bound (constant): H^ >= 2Q+2R (two-gap
+// path), E^/F^/h^+Q >= 3Q+2R, diagonal input + profile >= 2Q+minM, the
+// step-0 boundary input Q+4R; it fixes base.  Upper bound:
+// H^ <= min(m, n+1) maxM + (m+n)|R| (+ one profile value and 2|R| for the
+// diagonal input); it limits n.  Returns the largest admissible n (0 when the
+// query cannot use the f16 path at all) and the base.
 static uint32_t nw_f16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM, uint32_t* base) {
     *base = 0;
     if (Q > 0 || R > 0) return 0;
     const int64_t up = std::max<int64_t>(maxM, 0), lo = std::min<int64_t>(minM, 0);
-    const int64_t U = (int64_t)(m + 1) * up;
-    if (U > 0x77FF - 64) return 0;
-    const int64_t b = 0x7BFF - U;
+    const int64_t L = std::min({3 * (int64_t)Q + 2 * (int64_t)R, 2 * (int64_t)Q + lo, (int64_t)Q + 4 * (int64_t)R,
+                                2 * (int64_t)R}) - 2;
+    const int64_t b = 0x0400 - L;
     auto ok = [&](uint64_t n) {
-        const int64_t L = 3 * (int64_t)Q + (int64_t)(m + n + 4) * R + lo;
-        return L + b >= 0x0400;
+        const int64_t U = (int64_t)std::min<uint64_t>(m, n + 1) * up + (int64_t)(m + n + 2) * (-(int64_t)R) + up + 2;
+        return U + b <= 0x7BFF;
     };
     if (!ok(0)) return 0;
     *base = (uint32_t)b;
-    if (R == 0) return 0xffffffffu;
+    if (R == 0 && ok(0xffffffffull)) return 0xffffffffu;
     uint64_t a = 0, c = 0xffffffffull;
     while (c - a > 1) {
         const uint64_t x = (a + c) / 2;
@@ -672,7 +676,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // pair table of a strip of height 2P from row i0,
         //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
-        const int16_t padv = nw ? 0 : (use_f16 ? -1024 : -32768);
+        // NW on the pair kernel is diagonal-relative: every profile value (and
+        // the padding value 0) carries -2R
+        const int rel = use_nwf16 ? -2 * R : 0;
+        const int16_t padv = nw ? (int16_t)rel : (use_f16 ? -1024 : -32768);
         // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
         // rows up to the last strip's end so table builders need no bounds test
         const size_t mpad = std::max<size_t>((size_t)nstrips * 2 * np, m + 2 * pnp) + 64;
@@ -681,7 +688,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             const int64_t* row = M + ((size_t)D.code_of[c] << 5);
             uint16_t* pc = P.data() + (size_t)c * mpad;
             for (size_t i = 0; i < m; i++)
-                pc[i] = (uint16_t)(int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, row[qv.seq[i]]));
+                pc[i] = (uint16_t)(int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, row[qv.seq[i]] + rel));
         }
         auto prow_of = [&](uint32_t c) { return P.data() + (size_t)std::min(c, A) * mpad; };
         auto val = [&](uint32_t c, size_t i) -> int16_t { return (int16_t)prow_of(c)[i]; };

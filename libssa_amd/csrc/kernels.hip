@@ -426,10 +426,14 @@ strip_f16m_kernel(const StripArgs a) {
 //
 // Values are 16-bit patterns v + base that order like the positive f16
 // numbers they encode (see strip_f16m_kernel): SW uses base = kF16Floor and
-// the local-alignment floor inside E's max3; NW uses base = a.nw_base, chosen
-// on the host so that every real value and intermediate of entries up to
-// a.nmax16 columns stays inside [0x0400, 0x7BFF] -- NW needs
-// no floor and no saturation.  Padding rows/columns may leave that range;
+// the local-alignment floor inside E's max3.  NW works on diagonal-relative
+// values X^(i,j) = X(i,j) - (i+j)R: the gap-extension adds
+// of E and F cancel (E^ <- max(E^, h^+Q), F^ <- max(F^, h^+Q)), the profile
+// carries -2R, all boundaries become constants, and the score is
+// H^(m-1,len-1) + (m+len-2)R.  Its base a.nw_base is chosen on the host so
+// that every real value and intermediate of entries up to a.nmax16 columns
+// stays inside [0x0400, 0x7BFF] -- NW needs no floor and no
+// saturation.  Padding rows/columns may leave that range;
 // nothing real depends on them (dependencies only run down and right, and a
 // borrow only runs from a low half into the high half, whose cell is at the
 // same or a later column and row).
@@ -485,6 +489,7 @@ pair_kernel(const StripArgs a) {
     const int BASE = NW ? (int)a.nw_base : kF16Floor;
     const uint32_t cQR = (uint32_t)(QR * 65536 + QR);   // "combined" packed constants:
     const uint32_t cR = (uint32_t)(R * 65536 + R);      // one v_add_u32 updates both halves
+    const uint32_t cQ = (uint32_t)(Q * 65536 + Q);
     auto pat = [&](int v) -> uint32_t { return (uint32_t)(v + BASE) & 0xffffu; };
 
     uint32_t S = FL;
@@ -511,23 +516,24 @@ pair_kernel(const StripArgs a) {
         const bool first = (i0 == 0);
         const bool capture = CAP && s == last;
 
-        // ---- left boundary (column -1): SW 0, NW H(i,-1)=Q+(i+1)R, E_in(i,0)=2Q+(i+2)R.
-        // NW, high halves: step 0 runs them over the virtual column -1, and
-        // the initial values make that step produce the true boundary of
-        // rows i0+NP.. by itself: diagonal input H(i,-1) plus the padding
-        // profile 0, E and F at the pattern minimum, so h = H(i,-1) and the
-        // E leaving it is h+Q+R.
+        // ---- left boundary (column -1).  SW: 0.  NW, diagonal-relative
+        // (X^(i,j) = X(i,j) - (i+j)R): H^(i,-1) = Q+2R, E^ into column 0 =
+        // 2Q+2R, H^(-1,j) = Q+2R, F^ into row 0 = 2Q+2R, H^(-1,-1) = 2R --
+        // constants.  High halves: step 0 runs them over the virtual column
+        // -1, and the initial values make that step produce the boundary by
+        // itself: diagonal input Q+4R plus the padding profile -2R, E and F at
+        // the pattern minimum, so h = Q+2R and E leaves it as h+Q.
         uint32_t H[NP], E[NP];
 #pragma unroll
         for (int r = 0; r < NP; r++) {
-            H[r] = NW ? pat(Q + (i0 + r + 1) * R) | (pat(Q + (i0 + NP + r + 2) * R) << 16) : FL;
-            E[r] = NW ? pat(2 * Q + (i0 + r + 2) * R) | (0x0400u << 16) : FL;
+            H[r] = NW ? pat(Q + 2 * R) | (pat(Q + 4 * R) << 16) : FL;
+            E[r] = NW ? pat(2 * Q + 2 * R) | (0x0400u << 16) : FL;
         }
         // diagonal input of row i0 at column 0, H(i0-1, -1); high half H(i0+NP, -1)
-        uint32_t hd0 = NW ? pat(first ? 0 : Q + i0 * R) | (pat(Q + (i0 + NP + 1) * R) << 16) : FL;
+        uint32_t hd0 = NW ? pat(first ? 2 * R : Q + 2 * R) | (pat(Q + 4 * R) << 16) : FL;
         uint32_t Fprev = NW ? 0x0400u : FL;
         // synthesized top boundary of the first strip: (H(-1,j), F into row 0)
-        uint32_t rbsyn = NW ? (pat(Q + R) | (pat(2 * Q + 2 * R) << 16)) : FL;
+        const uint32_t rbsyn = NW ? (pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16)) : FL;
 
         uint32_t ob[4] = {0, 0, 0, 0};
         uint4 rnext = resp[0];
@@ -570,7 +576,6 @@ pair_kernel(const StripArgs a) {
                     uint32_t rbv;
                     if (first) {
                         rbv = rbsyn;
-                        if (NW) rbsyn += cR;
                     } else {
                         rbv = qw[u];
                     }
@@ -581,9 +586,16 @@ pair_kernel(const StripArgs a) {
                         const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
                         hd = H[r];
                         H[r] = h;
-                        const uint32_t tt = h + cQR;
-                        E[r] = NW ? fmax2(E[r] + cR, tt) : fmax3(E[r] + cR, tt, FL);
-                        F = fmax2(F + cR, tt);
+                        if (NW) {
+                            // diagonal-relative: E and F need no extension add
+                            const uint32_t tt = h + cQ;
+                            E[r] = fmax2(E[r], tt);
+                            F = fmax2(F, tt);
+                        } else {
+                            const uint32_t tt = h + cQR;
+                            E[r] = fmax3(E[r] + cR, tt, FL);
+                            F = fmax2(F + cR, tt);
+                        }
                         if (!NW && (r & 1)) S = fmax3(S, H[r - 1], H[r]);
                     }
                     hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
@@ -631,7 +643,8 @@ pair_kernel(const StripArgs a) {
         ovf = ovf || smax >= 0x7C00u;
         score = (int32_t)smax - kF16Floor;
     } else {
-        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE;
+        // back from the diagonal-relative value: + (i + j) R at (m-1, len-1)
+        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE + ((int32_t)a.m + (int32_t)len - 2) * R;
     }
     if (ovf) {
         const uint32_t idx = atomicAdd(a.ovf_count, 1u);
