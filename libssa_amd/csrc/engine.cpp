@@ -592,6 +592,28 @@ static uint32_t nw_f16_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM,
     return (uint32_t)a;
 }
 
+// SW on the pair kernel: diagonal-relative patterns H + (i+j)|R| + 0x0800
+// must stay below 0x7BFF for every real cell and the +1 padding column:
+// H <= min(m,n) maxM, plus one profile value and 2|R| for the diagonal
+// input.  The lower side holds by construction (floor >= 0x0800, minM and
+// Q >= -1024).  Returns the largest admissible entry length (0: never).
+static uint32_t sw_rel_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM) {
+    if (Q > 0 || R > 0 || Q < -1024 || minM < -1024 || maxM > 1024) return 0;
+    const int64_t up = std::max<int64_t>(maxM, 0), rabs = -(int64_t)R;
+    auto ok = [&](uint64_t n) {
+        const int64_t U = (int64_t)std::min<uint64_t>(m, n) * up + (int64_t)(m + n + 4) * rabs + up + kF16Floor;
+        return U <= 0x7BFF;
+    };
+    if (!ok(0)) return 0;
+    if (R == 0) return 0xffffffffu;
+    uint64_t a = 0, c = 0xffffffffull;
+    while (c - a > 1) {
+        const uint64_t x = (a + c) / 2;
+        if (ok(x)) a = x; else c = x;
+    }
+    return (uint32_t)a;
+}
+
 void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out) {
     check(hipSetDevice(D.device), "hipSetDevice");
     const Config& C = cfg();
@@ -655,31 +677,34 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
         const int pnp = C.pair_np == 24 ? 24 : 16;
         const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
-        // NW on f16 patterns: only when no more than a handful of entries
-        // exceed its length bound (those are re-scored by the int64 kernel)
-        uint32_t nw_base = 0, nmax_f16 = 0;
-        bool use_nwf16 = false;
-        if (nw && C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
-            nmax_f16 = std::min(nw_f16_limit(m, Q, R, minM, maxM, &nw_base), nmax16);
-            if (nmax_f16 > 0) {
+        // pair kernel (diagonal-relative f16 patterns): only when no more than
+        // a handful of entries exceed its length bound (those are re-scored
+        // by the int64 kernel); otherwise the strip kernels
+        uint32_t nw_base = 0;
+        bool use_pair = false;
+        if (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
+            uint32_t lim = nw ? nw_f16_limit(m, Q, R, minM, maxM, &nw_base) : sw_rel_limit(m, Q, R, minM, maxM);
+            lim = std::min(lim, nmax16);
+            if (lim > 0) {
                 const size_t beyond = (size_t)(D.len_sorted.end() -
-                                               std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), nmax_f16));
-                use_nwf16 = beyond <= 64;
+                                               std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
+                if (beyond <= 64) {
+                    use_pair = true;
+                    nmax16 = lim;
+                }
             }
         }
-        if (use_nwf16) nmax16 = nmax_f16;
-        const bool use_f16 = (!nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024) || use_nwf16;
-        // pair-symbol profile (pair_kernel): (alpha+1)^2 rows in LDS
-        const bool use_pair = use_f16 && (use_nwf16 || (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax));
-
+        // SW on f16 patterns without the pair table (strip_f16m_kernel) needs
+        // non-positive gaps and scores within +-1024
+        const bool use_f16 = use_pair || (!nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024);
         // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
         // pair table of a strip of height 2P from row i0,
         //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
         const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
         // NW on the pair kernel is diagonal-relative: every profile value (and
         // the padding value 0) carries -2R
-        const int rel = use_nwf16 ? -2 * R : 0;
-        const int16_t padv = nw ? (int16_t)rel : (use_f16 ? -1024 : -32768);
+        const int rel = use_pair ? -2 * R : 0;
+        const int16_t padv = nw ? (int16_t)rel : (use_f16 ? (int16_t)(-1024 + rel) : -32768);
         // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
         // rows up to the last strip's end so table builders need no bounds test
         const size_t mpad = std::max<size_t>((size_t)nstrips * 2 * np, m + 2 * pnp) + 64;

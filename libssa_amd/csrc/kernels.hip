@@ -293,6 +293,10 @@ __device__ __forceinline__ uint32_t fmax2(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(h2, a),
                                                                       __builtin_bit_cast(h2, b)));
 }
+__device__ __forceinline__ uint32_t psubsat16(uint32_t a, uint32_t b) {   // v_pk_sub_u16 clamp
+    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)));
+}
 __device__ __forceinline__ uint32_t padd16(uint32_t a, uint32_t b) {   // v_pk_add_u16 (wrapping)
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, a) + __builtin_bit_cast(u2, b));
 }
@@ -485,14 +489,16 @@ pair_kernel(const StripArgs a) {
     const uint32_t len = a.lane_len[gl];
 
     constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;
-    const int Q = a.gap_open, R = a.gap_extend, QR = Q + R;
+    const int Q = a.gap_open, R = a.gap_extend;
     const int BASE = NW ? (int)a.nw_base : kF16Floor;
-    const uint32_t cQR = (uint32_t)(QR * 65536 + QR);   // "combined" packed constants:
-    const uint32_t cR = (uint32_t)(R * 65536 + R);      // one v_add_u32 updates both halves
-    const uint32_t cQ = (uint32_t)(Q * 65536 + Q);
+    const uint32_t cQ = (uint32_t)(Q * 65536 + Q);      // "combined": one v_add_u32 updates both halves
     auto pat = [&](int v) -> uint32_t { return (uint32_t)(v + BASE) & 0xffffu; };
 
-    uint32_t S = FL;
+    // SW: running max of x = sat(h - floor(next column)) = max(H - |R|, 0),
+    // an exact H_max + (-|R|) unless it is 0 (then the lane is re-scored)
+    const uint32_t Rabs = (uint32_t)(-R);
+    const uint32_t cRabs = Rabs * 0x10001u;
+    uint32_t S = 0;
     if (!NW && (a.flags & kPairCarryIn) && active) S = a.smax[gl];
     uint32_t cap = 0;
     const int R2 = 2 * NP;
@@ -523,17 +529,31 @@ pair_kernel(const StripArgs a) {
         // -1, and the initial values make that step produce the boundary by
         // itself: diagonal input Q+4R plus the padding profile -2R, E and F at
         // the pattern minimum, so h = Q+2R and E leaves it as h+Q.
-        uint32_t H[NP], E[NP];
+        // SW, also diagonal-relative: true 0 is the pattern of (i+j)|R|, so
+        // the local-alignment floor differs per row and column: fl[r] holds
+        // the floor of the next column for both halves of row r (wave-
+        // uniform, SGPRs, +|R| per column).  Boundary H(i,-1) = 0 ->
+        // (i-1)|R|; high halves at step 0: E at the boundary value, the
+        // diagonal input and F low, so h = (i-1)|R|.
+        uint32_t H[NP], E[NP], fl[NP];
 #pragma unroll
         for (int r = 0; r < NP; r++) {
-            H[r] = NW ? pat(Q + 2 * R) | (pat(Q + 4 * R) << 16) : FL;
-            E[r] = NW ? pat(2 * Q + 2 * R) | (0x0400u << 16) : FL;
+            if (NW) {
+                H[r] = pat(Q + 2 * R) | (pat(Q + 4 * R) << 16);
+                E[r] = pat(2 * Q + 2 * R) | (0x0400u << 16);
+            } else {
+                H[r] = pat((i0 + r - 1) * (int)Rabs) | (pat(0) << 16);
+                E[r] = pat((i0 + r) * (int)Rabs) | (pat((i0 + NP + r - 1) * (int)Rabs) << 16);
+                fl[r] = __builtin_amdgcn_readfirstlane(pat((i0 + r + 1) * (int)Rabs) |
+                                                       (pat((i0 + NP + r) * (int)Rabs) << 16));
+            }
         }
-        // diagonal input of row i0 at column 0, H(i0-1, -1); high half H(i0+NP, -1)
-        uint32_t hd0 = NW ? pat(first ? 2 * R : Q + 2 * R) | (pat(Q + 4 * R) << 16) : FL;
-        uint32_t Fprev = NW ? 0x0400u : FL;
+        // diagonal input of row i0 at column 0, H(i0-1, -1); high half low
+        uint32_t hd0 = NW ? pat(first ? 2 * R : Q + 2 * R) | (pat(Q + 4 * R) << 16)
+                          : pat((i0 - 2) * (int)Rabs) | (pat(0) << 16);
+        uint32_t Fprev = 0x0400u;
         // synthesized top boundary of the first strip: (H(-1,j), F into row 0)
-        const uint32_t rbsyn = NW ? (pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16)) : FL;
+        uint32_t rbsyn = NW ? (pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16)) : pat(-(int)Rabs) * 0x10001u;
 
         uint32_t ob[4] = {0, 0, 0, 0};
         uint4 rnext = resp[0];
@@ -576,11 +596,13 @@ pair_kernel(const StripArgs a) {
                     uint32_t rbv;
                     if (first) {
                         rbv = rbsyn;
+                        if (!NW) rbsyn += cRabs;
                     } else {
                         rbv = qw[u];
                     }
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
+                    uint32_t xs[2];
 #pragma unroll
                     for (int r = 0; r < NP; r++) {
                         const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
@@ -592,11 +614,17 @@ pair_kernel(const StripArgs a) {
                             E[r] = fmax2(E[r], tt);
                             F = fmax2(F, tt);
                         } else {
-                            const uint32_t tt = h + cQR;
-                            E[r] = fmax3(E[r] + cR, tt, FL);
-                            F = fmax2(F + cR, tt);
+                            const uint32_t tt = h + cQ;
+                            E[r] = fmax3(E[r], tt, fl[r]);
+                            F = fmax2(F, tt);
+                            // x = max(H - |R|, 0) into H[r]'s slot of the S tree
+                            xs[r & 1] = psubsat16(h, fl[r]);
+                            if (r & 1) S = fmax3(S, xs[0], xs[1]);
                         }
-                        if (!NW && (r & 1)) S = fmax3(S, H[r - 1], H[r]);
+                    }
+                    if (!NW) {
+#pragma unroll
+                        for (int r = 0; r < NP; r++) fl[r] += cRabs;
                     }
                     hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
                     Fprev = F;
@@ -640,8 +668,9 @@ pair_kernel(const StripArgs a) {
     if (!NW) {
         const uint32_t slo = S & 0xffffu, shi = S >> 16;
         const uint32_t smax = slo > shi ? slo : shi;
-        ovf = ovf || smax >= 0x7C00u;
-        score = (int32_t)smax - kF16Floor;
+        // 0 leaves H_max in [0, |R|] undecided: re-score exactly
+        ovf = ovf || (smax == 0 && Rabs != 0);
+        score = (int32_t)smax + (int32_t)Rabs;
     } else {
         // back from the diagonal-relative value: + (i + j) R at (m-1, len-1)
         score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE + ((int32_t)a.m + (int32_t)len - 2) * R;
