@@ -40,9 +40,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU instructions per cell of each scoring kernel (all its launches of a
 # search), from PMC SQ_INSTS_VALU x 64 lanes / cells over the C2 (SW) and C3
 # (NW) searches: profiles/r01/pmc_c2_sw_np16 (strip16), pmc_c2_r01b and
-# pmc_c3_r01b (32-row pair strips), pmc_c2_np24 and pmc_c3_np24 (48-row strips,
-# the default: these values)
-VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 4.02, "pair_f16_nw": 3.87}
+# pmc_c3_r01b (32-row pair strips), pmc_c2_np24 / pmc_c3_np24 (48-row strips),
+# pmc_c2_rel / pmc_c3_rel (48-row strips, diagonal-relative values: the
+# default, these values)
+VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 3.54, "pair_f16_nw": 2.80}
 
 
 def parse():
