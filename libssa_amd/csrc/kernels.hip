@@ -557,7 +557,13 @@ pair_kernel(const StripArgs a) {
 
         uint32_t ob[4] = {0, 0, 0, 0};
         uint4 rnext = resp[0];
-        uint4 qnext = first ? make_uint4(0, 0, 0, 0) : rbp[0];
+        // row-buffer quads prefetched PF quads ahead (NW's shorter steps
+        // need the longer distance to cover HBM latency)
+        constexpr int PF = NW ? 2 : 1;
+        uint4 qn[PF];
+#pragma unroll
+        for (int p = 0; p < PF; p++)
+            qn[p] = (first || (uint32_t)p >= nquads) ? make_uint4(0, 0, 0, 0) : rbp[(size_t)p * 64];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
         uint32_t dprev = a.alpha;
         uint32_t nxt[NP];
@@ -574,10 +580,12 @@ pair_kernel(const StripArgs a) {
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 if (b * 4 + t >= nquads) break;      // uniform: the group's last columns
-                const uint4 qcur = qnext;
+                const uint4 qcur = qn[0];
+#pragma unroll
+                for (int p = 0; p + 1 < PF; p++) qn[p] = qn[p + 1];
                 if (!first) {
-                    const uint32_t nq = b * 4 + t + 1;
-                    if (nq < nquads) qnext = rbp[(size_t)nq * 64];
+                    const uint32_t nq = b * 4 + t + PF;
+                    if (nq < nquads) qn[PF - 1] = rbp[(size_t)nq * 64];
                 }
                 const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
 #pragma unroll
