@@ -44,7 +44,7 @@ void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
-    dfree(d_work); dfree(d_smax);
+    dfree(d_work);
     dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
     if (h_fbuf) (void)hipHostFree(h_fbuf);
     if (h_up) (void)hipHostFree(h_up);
@@ -58,7 +58,7 @@ void DeviceDB::release() {
     if (h_wide) (void)hipHostFree(h_wide);
     d_groups = nullptr; d_res = nullptr; d_rowbuf = nullptr; d_lane_len = nullptr; d_lane_out = nullptr;
     d_scores = nullptr; d_ovf = nullptr; d_wide = nullptr; d_qpt = nullptr; d_query = nullptr;
-    d_matrix = nullptr; d_work = nullptr; d_smax = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
+    d_matrix = nullptr; d_work = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
     h_scores_cap = qpt_cap = query_cap = work_cap = 0;
     generation = ~0ull;
     meta = EntryMeta();
@@ -317,7 +317,6 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     dalloc((void**)&D.d_rowbuf, H.res.size() * 4, "row buffer");
     dalloc((void**)&D.d_lane_len, H.lane_len.size() * 4, "lane_len");
     dalloc((void**)&D.d_lane_out, H.lane_out.size() * 4, "lane_out");
-    dalloc((void**)&D.d_smax, H.lane_out.size() * 4, "running max");
     {
         const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
         dalloc((void**)&D.d_fbuf, 16 + std::max<size_t>(E, 1) * 8, "filter candidates");
@@ -717,24 +716,30 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         auto prow_of = [&](uint32_t c) { return P.data() + (size_t)std::min(c, A) * mpad; };
         auto val = [&](uint32_t c, size_t i) -> int16_t { return (int16_t)prow_of(c)[i]; };
-        struct PairLaunch { int np; uint32_t row0, nstrips; size_t qoff; uint32_t flags; bool cap; };
-        std::vector<PairLaunch> plan;
+        // pair kernel plan (one launch): main strips of 2*pnp rows, then a
+        // tail strip of the smallest height that holds the remainder (16 rows:
+        // 8, 32: 16); NW always ends in a tail strip, which captures its score
         std::vector<uint32_t> qpt;
+        uint32_t main_strips = 0;
+        int tail_np = 0;
+        size_t tail_off = 0;
         if (use_pair) {
-            // main strips of 2*pnp rows; the remainder becomes one strip of
-            // the smallest height that holds it (16 rows: NP 8, 32: NP 16);
-            // NW's last strip runs as its own capture launch
             const uint32_t Hm = 2 * pnp;
-            const uint32_t full = (uint32_t)(m / Hm), rem = (uint32_t)(m % Hm);
-            std::vector<std::pair<int, uint32_t>> segs;   // (np, strips)
-            if (rem == 0) segs = {{pnp, full}};
-            else if (rem <= 16) segs = {{pnp, full}, {8, 1}};
-            else if (rem <= 32 && pnp > 16) segs = {{pnp, full}, {16, 1}};
-            else segs = {{pnp, full + 1}};
-            if (nw && segs.back().second > 1) {
-                const int snp = segs.back().first;
-                segs.back().second--;
-                segs.push_back({snp, 1});
+            uint32_t full = (uint32_t)(m / Hm);
+            const uint32_t rem = (uint32_t)(m % Hm);
+            if (rem == 0) {
+                if (nw) {
+                    full--;
+                    tail_np = pnp;
+                }
+            } else if (rem <= 16) {
+                tail_np = 8;
+            } else if (rem <= 32 && pnp > 16) {
+                tail_np = 16;
+            } else if (nw) {
+                tail_np = pnp;
+            } else {
+                full++;     // SW: the remainder as one more (padded) main strip
             }
             auto add_tables = [&](int Ph, uint32_t row0, uint32_t count) {
                 const size_t off = qpt.size();
@@ -752,18 +757,9 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
                 return off;
             };
-            uint32_t row0 = 0;
-            for (size_t g = 0; g < segs.size(); g++) {
-                const auto [snp, cnt] = segs[g];
-                if (cnt == 0) continue;
-                const bool cap = nw && g + 1 == segs.size();
-                plan.push_back({snp, row0, cnt, add_tables(snp, row0, cnt), 0, cap});
-                row0 += cnt * 2 * snp;
-            }
-            for (size_t l = 0; l < plan.size(); l++) {
-                if (l > 0) plan[l].flags |= kPairCarryIn;
-                if (l + 1 == plan.size()) plan[l].flags |= kPairFinal;
-            }
+            main_strips = full;
+            add_tables(pnp, 0, full);
+            if (tail_np) tail_off = add_tables(tail_np, full * Hm, 1);
         } else {
             qpt.resize((size_t)nstrips * 32 * np);
             for (uint32_t s = 0; s < nstrips; s++)
@@ -835,7 +831,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
         a.alpha = A;
         a.nw_base = nw_base;
-        a.smax = D.d_smax;
 
         WideArgs w{};
         w.res = D.d_res;
@@ -859,14 +854,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (v == 0) prep = now_ms() - t_prep0;
         check(hipEventRecord(D.ev[0], st), "event");
         if (use_pair) {
-            for (const PairLaunch& l : plan) {
-                StripArgs b = a;
-                b.qpt = D.d_qpt + l.qoff;
-                b.row0 = l.row0;
-                b.nstrips = l.nstrips;
-                b.flags = l.flags;
-                check(launch_pair(b, l.np, nw, l.cap, (size_t)prow * prow * (l.np + 4) * 4, st), "pair kernel launch");
-            }
+            StripArgs b = a;
+            b.nstrips = main_strips;
+            b.qpt_tail = D.d_qpt + tail_off;
+            const int lnp = main_strips ? pnp : tail_np;
+            check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }

@@ -37,7 +37,6 @@ struct DeviceDB {
     uint4* d_rowbuf = nullptr;
     uint32_t* d_lane_len = nullptr;
     uint32_t* d_lane_out = nullptr;
-    uint32_t* d_smax = nullptr;           // SW running max between pair_kernel launches
     // top-k candidate filter (kernels.h FilterArgs)
     uint32_t* d_fbuf = nullptr;           // [4] counters, then (index, score) x entries
     int32_t* d_summary = nullptr;

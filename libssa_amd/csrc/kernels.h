@@ -32,14 +32,9 @@ struct StripArgs {
     uint32_t pad_word;         // profile dword of the padding residue (both halves)
     uint32_t alpha;            // compact alphabet size; code alpha = padding column
     uint32_t nw_base;          // NW pattern offset of pair_kernel (value + nw_base)
-    // pair_kernel launches (engine.cpp plans them): a.nstrips strips from
-    // query row row0, tables at qpt; flags below; SW running max carried in smax
-    uint32_t row0;
-    uint32_t flags;
-    uint32_t* smax;            // [ngroups * 64]
+    // pair_kernel: the tail strip's table (launch_pair's npt > 0)
+    const uint32_t* qpt_tail;
 };
-constexpr uint32_t kPairFinal = 1;      // this launch holds the query's last row: write scores
-constexpr uint32_t kPairCarryIn = 2;    // SW: start from the running max in smax
 
 struct WideArgs {
     const uint4* res;
@@ -80,7 +75,9 @@ hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
-hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st);
+// a.nstrips strips of 2*np rows, then one of 2*npt rows (npt 0: none;
+// required for NW, whose score is captured in the last strip)
+hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
 }  // namespace ssa

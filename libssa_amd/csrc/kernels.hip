@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace ssa {
@@ -452,24 +454,25 @@ strip_f16m_kernel(const StripArgs a) {
 // barrier per strip; groups of a workgroup are adjacent in the length order,
 // so their strips take nearly the same time).
 //
-// One launch covers a.nstrips strips starting at query row a.row0 (the host
-// plans the launches, engine.cpp): the bulk of the query in 32-row strips
-// (NP = 16), a remainder of <= 16 rows as one NP = 8 strip instead of a
-// half-empty 32-row one, and for NW the last strip in its own CAP launch:
-// capturing H(m-1, len-1) costs a 16-way select per column, and in the same
-// instantiation it raised the register allocation of the code every other
-// strip runs (past 128 VGPRs: spills).  SW carries its running maximum from
-// one launch to the next through a.smax.
+// One launch covers the whole query: a.nstrips strips of 2*NP rows from row
+// 0, then -- when NPT > 0 -- one final strip of 2*NPT rows with its own table
+// (a.qpt_tail).  The host (engine.cpp) picks NPT as the smallest height that
+// holds the remainder (16 rows: NPT = 8, 32: 16), so a 400-row query runs 8
+// strips of 48 rows and one of 16 instead of a half-empty 48-row strip, and
+// without a second launch (a separate launch of the short strip cost its
+// own grid ramp and prologue: ~20 % above its instruction count).  NW always
+// runs its last strip as the tail: it captures H(m-1, len-1), a per-column
+// select that only the tail's instantiation carries (in the main strips'
+// code it raised the register allocation past the 3-waves limit).
 //
 // Columns are processed up to GroupDesc::ncols (a multiple of 4, >= the
 // group's longest entry + 1) in 16-column residue blocks with a uniform exit
 // inside the last block.
 // ---------------------------------------------------------------------------
-template <int NP, bool NW, bool CAP>
+template <int NP, bool NW, int NPT>
 __global__ void __launch_bounds__(64 * kPairWaves, NP <= 16 ? 4 : 3)
 pair_kernel(const StripArgs a) {
     constexpr int W = kPairWaves;
-    constexpr int ROWW = NP + 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
     const int lane = threadIdx.x & 63;
@@ -485,7 +488,6 @@ pair_kernel(const StripArgs a) {
     uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
     const uint32_t gl = gg * 64 + lane;
     const uint32_t prow = a.alpha + 1;
-    const uint32_t ntab4 = prow * prow * (NP / 4);  // 16-B chunks per strip table
     const uint32_t len = a.lane_len[gl];
 
     constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;
@@ -499,28 +501,31 @@ pair_kernel(const StripArgs a) {
     const uint32_t Rabs = (uint32_t)(-R);
     const uint32_t cRabs = Rabs * 0x10001u;
     uint32_t S = 0;
-    if (!NW && (a.flags & kPairCarryIn) && active) S = a.smax[gl];
+    // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
     uint32_t cap = 0;
-    const int R2 = 2 * NP;
-    const int last = (int)a.nstrips - 1;
-    const int rr = (int)a.m - 1 - ((int)a.row0 + last * R2);   // strip row of the last query row
-    const int cap_half = rr >= NP ? 1 : 0;
-    const int cap_row = rr - cap_half * NP;
-    const uint32_t cap_col = len - 1 + cap_half;
+    int cap_half = 0;
 
-    for (int s = 0; s < (int)a.nstrips; s++) {
+    // One strip of height 2*NPS from query row i0, table at src.  CAPS: the
+    // strip holding row m-1 of an NW search (captures its H).
+    auto strip = [&](auto np_c, auto cap_c, int i0, const uint32_t* tab) {
+        constexpr int NPS = decltype(np_c)::value;
+        constexpr bool CAPS = decltype(cap_c)::value;
+        constexpr int ROWW = NPS + 4;
         // ---- the whole workgroup stages this strip's pair table
         __syncthreads();
-        const uint4* src = (const uint4*)(a.qpt + (size_t)s * prow * prow * NP);
+        const uint32_t ntab4 = prow * prow * (NPS / 4);
+        const uint4* src = (const uint4*)tab;
         for (uint32_t i = threadIdx.x; i < ntab4; i += 64 * W) {
-            const uint32_t row = i / (NP / 4), k = i % (NP / 4);
+            const uint32_t row = i / (NPS / 4), k = i % (NPS / 4);
             *(uint4*)(lds + row * ROWW + 4 * k) = src[i];
         }
         __syncthreads();
-        if (!active) continue;
-        const int i0 = (int)a.row0 + s * R2;    // first query row of the strip
+        if (!active) return;
         const bool first = (i0 == 0);
-        const bool capture = CAP && s == last;
+        const int rr = (int)a.m - 1 - i0;        // strip row of the last query row (CAPS)
+        if (CAPS) cap_half = rr >= NPS ? 1 : 0;
+        const int cap_row = rr - cap_half * NPS;
+        const uint32_t cap_col = len - 1 + cap_half;
 
         // ---- left boundary (column -1).  SW: 0.  NW, diagonal-relative
         // (X^(i,j) = X(i,j) - (i+j)R): H^(i,-1) = Q+2R, E^ into column 0 =
@@ -535,17 +540,17 @@ pair_kernel(const StripArgs a) {
         // uniform, SGPRs, +|R| per column).  Boundary H(i,-1) = 0 ->
         // (i-1)|R|; high halves at step 0: E at the boundary value, the
         // diagonal input and F low, so h = (i-1)|R|.
-        uint32_t H[NP], E[NP], fl[NP];
+        uint32_t H[NPS], E[NPS], fl[NPS];
 #pragma unroll
-        for (int r = 0; r < NP; r++) {
+        for (int r = 0; r < NPS; r++) {
             if (NW) {
                 H[r] = pat(Q + 2 * R) | (pat(Q + 4 * R) << 16);
                 E[r] = pat(2 * Q + 2 * R) | (0x0400u << 16);
             } else {
                 H[r] = pat((i0 + r - 1) * (int)Rabs) | (pat(0) << 16);
-                E[r] = pat((i0 + r) * (int)Rabs) | (pat((i0 + NP + r - 1) * (int)Rabs) << 16);
+                E[r] = pat((i0 + r) * (int)Rabs) | (pat((i0 + NPS + r - 1) * (int)Rabs) << 16);
                 fl[r] = __builtin_amdgcn_readfirstlane(pat((i0 + r + 1) * (int)Rabs) |
-                                                       (pat((i0 + NP + r) * (int)Rabs) << 16));
+                                                       (pat((i0 + NPS + r) * (int)Rabs) << 16));
             }
         }
         // diagonal input of row i0 at column 0, H(i0-1, -1); high half low
@@ -566,10 +571,10 @@ pair_kernel(const StripArgs a) {
             qn[p] = (first || (uint32_t)p >= nquads) ? make_uint4(0, 0, 0, 0) : rbp[(size_t)p * 64];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
         uint32_t dprev = a.alpha;
-        uint32_t nxt[NP];
+        uint32_t nxt[NPS];
         {
             const uint32_t d0 = rnext.x & 0xffu;
-            load_row<NP>(nxt, lds + (d0 * prow + dprev) * ROWW);
+            load_row<NPS>(nxt, lds + (d0 * prow + dprev) * ROWW);
             dprev = d0;
         }
 
@@ -592,13 +597,13 @@ pair_kernel(const StripArgs a) {
                 for (int u = 0; u < 4; u++) {
                     const int k = t * 4 + u;
                     const uint32_t j = b * 16 + k;
-                    uint32_t P[NP];
+                    uint32_t P[NPS];
 #pragma unroll
-                    for (int r = 0; r < NP; r++) P[r] = nxt[r];
+                    for (int r = 0; r < NPS; r++) P[r] = nxt[r];
                     {
                         const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
                                                    : (rnext.x & 0xffu);
-                        load_row<NP>(nxt, lds + (dn * prow + dprev) * ROWW);
+                        load_row<NPS>(nxt, lds + (dn * prow + dprev) * ROWW);
                         dprev = dn;
                     }
                     uint32_t rbv;
@@ -612,7 +617,7 @@ pair_kernel(const StripArgs a) {
                     uint32_t hd = hd0;
                     uint32_t xs[2];
 #pragma unroll
-                    for (int r = 0; r < NP; r++) {
+                    for (int r = 0; r < NPS; r++) {
                         const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
                         hd = H[r];
                         H[r] = h;
@@ -632,7 +637,7 @@ pair_kernel(const StripArgs a) {
                     }
                     if (!NW) {
 #pragma unroll
-                        for (int r = 0; r < NP; r++) fl[r] += cRabs;
+                        for (int r = 0; r < NPS; r++) fl[r] += cRabs;
                     }
                     hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
                     Fprev = F;
@@ -642,14 +647,14 @@ pair_kernel(const StripArgs a) {
                     else asm volatile("" : "+v"(Fprev));
                     // step 0's high half is the virtual column -1: no output
                     if (b != 0 || k != 0) {
-                        ob[(k + 3) & 3] = perm(F, H[NP - 1], SEL_LO_BHI_HI_AHI);
+                        ob[(k + 3) & 3] = perm(F, H[NPS - 1], SEL_LO_BHI_HI_AHI);
                         if ((k & 3) == 0)
                             rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
                     }
-                    if (capture) {
+                    if (CAPS) {
                         uint32_t hsel = H[0];
 #pragma unroll
-                        for (int r = 1; r < NP; r++) hsel = (cap_row == r) ? H[r] : hsel;
+                        for (int r = 1; r < NPS; r++) hsel = (cap_row == r) ? H[r] : hsel;
                         cap = (j == cap_col) ? hsel : cap;
                     }
                     __builtin_amdgcn_sched_barrier(0);
@@ -658,13 +663,16 @@ pair_kernel(const StripArgs a) {
         }
         ob[3] = FL;
         rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-    }
+    };
+
+    using MainNP = std::integral_constant<int, NP>;
+    using TailNP = std::integral_constant<int, NPT ? NPT : 8>;
+    for (int s = 0; s < (int)a.nstrips; s++)
+        strip(MainNP{}, std::false_type{}, s * 2 * NP, a.qpt + (size_t)s * prow * prow * NP);
+    if (NPT > 0)
+        strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, a.qpt_tail);
 
     if (!active) return;
-    if (!(a.flags & kPairFinal)) {
-        if (!NW) a.smax[gl] = S;
-        return;
-    }
     const uint32_t o = a.lane_out[gl];
     if (o == 0xffffffffu) return;
     if (len == 0) {
@@ -937,32 +945,41 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int NP, bool NW, bool CAP>
+template <int NP, bool NW, int NPT>
 static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<NP, NW, CAP>,
+        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<NP, NW, NPT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLdsMax);
         if (e != hipSuccess) return e;
         attr = true;
     }
     const uint32_t blocks = (a.ngroups + kPairWaves - 1) / kPairWaves;
-    hipLaunchKernelGGL((pair_kernel<NP, NW, CAP>), dim3(blocks), dim3(64 * kPairWaves), lds_bytes, st, a);
+    hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * kPairWaves), lds_bytes, st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_pair(const StripArgs& a, int np, bool nw, bool cap, size_t lds_bytes, hipStream_t st) {
-    if (a.ngroups == 0 || a.nstrips == 0) return hipSuccess;
-    if (np == 24) {
-        if (!nw) return launch_pair_t<24, false, false>(a, lds_bytes, st);
-        return cap ? launch_pair_t<24, true, true>(a, lds_bytes, st) : launch_pair_t<24, true, false>(a, lds_bytes, st);
+template <int NP, bool NW>
+static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st) {
+    if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st);
+    if (npt == 8) return launch_pair_t<NP, NW, 8>(a, lds_bytes, st);
+    if constexpr (NP >= 16) {
+        if (npt == 16) return launch_pair_t<NP, NW, 16>(a, lds_bytes, st);
     }
-    if (np == 8) {
-        if (!nw) return launch_pair_t<8, false, false>(a, lds_bytes, st);
-        return cap ? launch_pair_t<8, true, true>(a, lds_bytes, st) : launch_pair_t<8, true, false>(a, lds_bytes, st);
+    if constexpr (NP >= 24) {
+        if (npt == 24) return launch_pair_t<NP, NW, 24>(a, lds_bytes, st);
     }
-    if (!nw) return launch_pair_t<16, false, false>(a, lds_bytes, st);
-    return cap ? launch_pair_t<16, true, true>(a, lds_bytes, st) : launch_pair_t<16, true, false>(a, lds_bytes, st);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st) {
+    if (a.ngroups == 0 || (a.nstrips == 0 && npt == 0)) return hipSuccess;
+    // NW scores come from the tail strip's capture
+    if (nw && npt == 0) return hipErrorInvalidValue;
+    if (np == 24) return nw ? launch_pair_np<24, true>(a, npt, lds_bytes, st) : launch_pair_np<24, false>(a, npt, lds_bytes, st);
+    if (np == 16) return nw ? launch_pair_np<16, true>(a, npt, lds_bytes, st) : launch_pair_np<16, false>(a, npt, lds_bytes, st);
+    if (np == 8) return nw ? launch_pair_np<8, true>(a, npt, lds_bytes, st) : launch_pair_np<8, false>(a, npt, lds_bytes, st);
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {
