@@ -522,10 +522,24 @@ pair_kernel(const StripArgs a) {
         __syncthreads();
         if (!active) return;
         const bool first = (i0 == 0);
+        // the last strip's boundary row has no reader
+        const bool keep = i0 + 2 * NPS < (int)a.m;
         const int rr = (int)a.m - 1 - i0;        // strip row of the last query row (CAPS)
         if (CAPS) cap_half = rr >= NPS ? 1 : 0;
         const int cap_row = rr - cap_half * NPS;
         const uint32_t cap_col = len - 1 + cap_half;
+        // the wave's capture columns span [cmin, cmax] (lengths are sorted, so
+        // the span is narrow): the select runs only there, behind a scalar test
+        uint32_t cmin = 0, cmax = 0;
+        if (CAPS) {
+            uint32_t lo = len ? cap_col : 0xffffffffu, hi = len ? cap_col : 0u;
+            for (int o = 32; o > 0; o >>= 1) {
+                lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+                hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+            }
+            cmin = __builtin_amdgcn_readfirstlane(lo);
+            cmax = __builtin_amdgcn_readfirstlane(hi);
+        }
 
         // ---- left boundary (column -1).  SW: 0.  NW, diagonal-relative
         // (X^(i,j) = X(i,j) - (i+j)R): H^(i,-1) = Q+2R, E^ into column 0 =
@@ -648,10 +662,10 @@ pair_kernel(const StripArgs a) {
                     // step 0's high half is the virtual column -1: no output
                     if (b != 0 || k != 0) {
                         ob[(k + 3) & 3] = perm(F, H[NPS - 1], SEL_LO_BHI_HI_AHI);
-                        if ((k & 3) == 0)
+                        if ((k & 3) == 0 && keep)
                             rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
                     }
-                    if (CAPS) {
+                    if (CAPS && j >= cmin && j <= cmax) {
                         uint32_t hsel = H[0];
 #pragma unroll
                         for (int r = 1; r < NPS; r++) hsel = (cap_row == r) ? H[r] : hsel;
@@ -662,7 +676,7 @@ pair_kernel(const StripArgs a) {
             }
         }
         ob[3] = FL;
-        rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        if (keep) rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
     };
 
     using MainNP = std::integral_constant<int, NP>;

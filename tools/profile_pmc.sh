@@ -5,6 +5,7 @@
 #             domains other than --kernel-trace)
 # Usage (on the box, from the repo root):
 #   tools/profile_pmc.sh <out_dir> [bench args...]
+# PASSES="stats fetch write" limits the passes (default: all)
 set -e -o pipefail
 OUT=$(realpath -m "$1"); shift
 REPO=$(cd "$(dirname "$0")/.." && pwd)
@@ -12,8 +13,10 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
+PASSES=${PASSES:-"stats fetch write valu wait lds icache"}
 run() {   # name, rocprof args...
     local name=$1; shift
+    case " $PASSES " in *" $name "*) ;; *) return 0 ;; esac
     timeout -k 10 300 rocprofv3 "$@" --kernel-include-regex "strip|pair" -d "$OUT/$name" -o run --output-format csv \
         -- python3 "$REPO/bench.py" $ARGS > "$OUT/$name.log" 2>&1
 }
