@@ -717,8 +717,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         auto prow_of = [&](uint32_t c) { return P.data() + (size_t)std::min(c, A) * mpad; };
         auto val = [&](uint32_t c, size_t i) -> int16_t { return (int16_t)prow_of(c)[i]; };
         // pair kernel plan (one launch): main strips of 2*pnp rows, then a
-        // tail strip of the smallest height that holds the remainder (16 rows:
-        // 8, 32: 16); NW always ends in a tail strip, which captures its score
+        // tail strip of the smallest height (multiple of 8 rows) that holds the
+        // remainder; NW always ends in a tail strip, which captures its score
         std::vector<uint32_t> qpt;
         uint32_t main_strips = 0;
         int tail_np = 0;
@@ -727,19 +727,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             const uint32_t Hm = 2 * pnp;
             uint32_t full = (uint32_t)(m / Hm);
             const uint32_t rem = (uint32_t)(m % Hm);
-            if (rem == 0) {
-                if (nw) {
-                    full--;
-                    tail_np = pnp;
-                }
-            } else if (rem <= 16) {
-                tail_np = 8;
-            } else if (rem <= 32 && pnp > 16) {
-                tail_np = 16;
+            if (rem > 0) {
+                tail_np = (int)(rem + 7) / 8 * 4;     // 8-row granularity
             } else if (nw) {
+                full--;
                 tail_np = pnp;
-            } else {
-                full++;     // SW: the remainder as one more (padded) main strip
             }
             auto add_tables = [&](int Ph, uint32_t row0, uint32_t count) {
                 const size_t off = qpt.size();

@@ -456,10 +456,10 @@ strip_f16m_kernel(const StripArgs a) {
 //
 // One launch covers the whole query: a.nstrips strips of 2*NP rows from row
 // 0, then -- when NPT > 0 -- one final strip of 2*NPT rows with its own table
-// (a.qpt_tail).  The host (engine.cpp) picks NPT as the smallest height that
-// holds the remainder (16 rows: NPT = 8, 32: 16), so a 400-row query runs 8
-// strips of 48 rows and one of 16 instead of a half-empty 48-row strip, and
-// without a second launch (a separate launch of the short strip cost its
+// (a.qpt_tail).  The host (engine.cpp) picks NPT as the smallest multiple of 4
+// (8 rows) that holds the remainder, so a 400-row query runs 8 strips of 48
+// rows and one of 16 instead of a half-empty 48-row strip, and without a
+// second launch (a separate launch of the short strip cost its
 // own grid ramp and prologue: ~20 % above its instruction count).  NW always
 // runs its last strip as the tail: it captures H(m-1, len-1), a per-column
 // select that only the tail's instantiation carries (in the main strips'
@@ -973,16 +973,14 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     return hipGetLastError();
 }
 
-template <int NP, bool NW>
+template <int NP, bool NW, int NPT = 4>
 static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st) {
-    if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st);
-    if (npt == 8) return launch_pair_t<NP, NW, 8>(a, lds_bytes, st);
-    if constexpr (NP >= 16) {
-        if (npt == 16) return launch_pair_t<NP, NW, 16>(a, lds_bytes, st);
+    // npt in {0} + multiples of 4 up to NP
+    if constexpr (NPT == 4) {
+        if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st);
     }
-    if constexpr (NP >= 24) {
-        if (npt == 24) return launch_pair_t<NP, NW, 24>(a, lds_bytes, st);
-    }
+    if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st);
+    if constexpr (NPT + 4 <= NP) return launch_pair_np<NP, NW, NPT + 4>(a, npt, lds_bytes, st);
     return hipErrorInvalidValue;
 }
 

@@ -114,7 +114,7 @@ def test_random_golden_full_score_vectors(fname):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 80, 81, 96, 97, 100])
+@pytest.mark.parametrize("qlen", [1, 2, 8, 9, 15, 16, 17, 24, 25, 31, 32, 33, 40, 41, 47, 48, 49, 63, 64, 65, 80, 81, 88, 89, 96, 97, 100])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_query_length_edges_vs_oracle(qlen, algo):
     rng = np.random.default_rng(qlen)
@@ -136,7 +136,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
             S.set_option("sw_kernel", swk)
             for np_ in (8, 16, 32):
                 S.set_option("strip_np", np_)
-                for pnp in ((16, 24) if swk == 0 and np_ == 16 else (24,)):
+                for pnp in ((8, 16, 24) if swk == 0 and np_ == 16 else (24,)):
                     S.set_option("pair_np", pnp)
                     sc, ids = _full_scores(qq, algo, len(keep))
                     assert (ids == keep).all()
