@@ -248,7 +248,7 @@ def main():
     # VALU issue roofline: the strip kernel is made of
     # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
     # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
-    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_c2_sw_np16).
+    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01c).
     instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 and args.pair_np == 24 else None
     issue_cycles = 4.17
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
@@ -272,7 +272,12 @@ def main():
                    "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_np": args.pair_np, "strip_np": args.strip_np,
                    "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     # the resource that actually binds this integer DP
+                     "binding": {"bound": "valu_issue",
+                                 "achieved": round(cells_local / (kavg * 1e-3) / 1e9, 2),
+                                 "peak": round(valu_bound / 1e9, 1) if valu_bound else None, "unit": "GCUPS",
+                                 "frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None}},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
                    "wide_ms_avg": round(float(np.mean(wide_ms)), 4),
