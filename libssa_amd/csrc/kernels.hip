@@ -469,10 +469,32 @@ strip_f16m_kernel(const StripArgs a) {
 // group's longest entry + 1) in 16-column residue blocks with a uniform exit
 // inside the last block.
 // ---------------------------------------------------------------------------
+// row groups of the SW anti-diagonal maxima: 16, then 8, then 4 rows
+constexpr int ad_size_at(int s, int np) { return np - s >= 16 ? 16 : (np - s >= 8 ? 8 : 4); }
+constexpr int ad_start(int r, int np) {
+    int s = 0;
+    while (r >= s + ad_size_at(s, np)) s += ad_size_at(s, np);
+    return s;
+}
+constexpr int ad_size(int r, int np) { return ad_size_at(ad_start(r, np), np); }
+constexpr int ad_index(int r, int np) {
+    int s = 0, i = 0;
+    while (r >= s + ad_size_at(s, np)) s += ad_size_at(s, np), i++;
+    return i;
+}
+constexpr int ad_ngroups(int np) { return ad_index(np - 1, np) + 1; }
+
+// waves per workgroup (they share the pair table) and waves per SIMD the
+// register budget is sized for.  (64-row strips, NP = 32, were tried: their
+// 63.5 KiB table allows two workgroups per CU, and at 3-4 waves/SIMD the
+// strip's state no longer fits the registers -- they spill in the DP loop.)
+constexpr int pair_waves(int, bool) { return kPairWaves; }
+constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : 3; }
+
 template <int NP, bool NW, int NPT>
-__global__ void __launch_bounds__(64 * kPairWaves, NP <= 16 ? 4 : 3)
+__global__ void __launch_bounds__(64 * pair_waves(NP, NW), pair_occupancy(NP, NW))
 pair_kernel(const StripArgs a) {
-    constexpr int W = kPairWaves;
+    constexpr int W = pair_waves(NP, NW);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
     const int lane = threadIdx.x & 63;
@@ -574,6 +596,27 @@ pair_kernel(const StripArgs a) {
         // synthesized top boundary of the first strip: (H(-1,j), F into row 0)
         uint32_t rbsyn = NW ? (pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16)) : pat(-(int)Rabs) * 0x10001u;
 
+        // SW, anti-diagonal maxima (AD): cells (r, j) and (r+1, j-1) have the
+        // same diagonal-relative offset i0+r+j, so the running maximum needs no
+        // per-cell floor subtraction when it is taken along anti-diagonals.
+        // The strip's rows are split into groups of 16/8/4 rows (ad_group);
+        // in a group of G rows from row g, A[g + (a - g) % G] collects
+        // anti-diagonal a: at column j every even local row adds its new h and
+        // the previous column's H of the row below (one max3 per two cells);
+        // the group's anti-diagonal g+j is complete after its first row at
+        // column j and is flushed into S with one saturating subtract of its
+        // floor (= that row's floor fl[g]).  G divides the 16-column block, so
+        // every register index is static.
+        constexpr bool AD = !NW;
+        // floors advance right after their row's last use (fewer live SGPRs;
+        // measured neutral at 16 rows, -0.7 % at 24, where they fit anyway)
+        constexpr bool FL_INROW = NPS <= 16;
+        constexpr int NG = ad_ngroups(NPS);
+        uint32_t A[AD ? NPS : 1];
+#pragma unroll
+        for (int p = 0; p < (AD ? NPS : 1); p++) A[p] = 0;
+        uint32_t xa[2] = {0, 0};
+
         uint32_t ob[4] = {0, 0, 0, 0};
         uint4 rnext = resp[0];
         // row-buffer quads prefetched PF quads ahead (NW's shorter steps
@@ -585,10 +628,15 @@ pair_kernel(const StripArgs a) {
             qn[p] = (first || (uint32_t)p >= nquads) ? make_uint4(0, 0, 0, 0) : rbp[(size_t)p * 64];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
         uint32_t dprev = a.alpha;
-        uint32_t nxt[NPS];
+        // P: the current column's profile operands.  INPLACE: the next
+        // column's row is loaded into P behind the row loop, four rows at a
+        // time (no second buffer: the registers pay for AD's accumulators)
+        constexpr bool INPLACE = true;
+        uint32_t P[NPS];
+        uint32_t nxt[NPS];   // unused when INPLACE
         {
             const uint32_t d0 = rnext.x & 0xffu;
-            load_row<NPS>(nxt, lds + (d0 * prow + dprev) * ROWW);
+            load_row<NPS>(INPLACE ? P : nxt, lds + (d0 * prow + dprev) * ROWW);
             dprev = d0;
         }
 
@@ -611,14 +659,17 @@ pair_kernel(const StripArgs a) {
                 for (int u = 0; u < 4; u++) {
                     const int k = t * 4 + u;
                     const uint32_t j = b * 16 + k;
-                    uint32_t P[NPS];
-#pragma unroll
-                    for (int r = 0; r < NPS; r++) P[r] = nxt[r];
+                    const uint32_t* nrow;
                     {
                         const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
                                                    : (rnext.x & 0xffu);
-                        load_row<NPS>(nxt, lds + (dn * prow + dprev) * ROWW);
+                        nrow = lds + (dn * prow + dprev) * ROWW;
                         dprev = dn;
+                    }
+                    if constexpr (!INPLACE) {
+#pragma unroll
+                        for (int r = 0; r < NPS; r++) P[r] = nxt[r];
+                        load_row<NPS>(nxt, nrow);
                     }
                     uint32_t rbv;
                     if (first) {
@@ -633,7 +684,20 @@ pair_kernel(const StripArgs a) {
 #pragma unroll
                     for (int r = 0; r < NPS; r++) {
                         const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
+                        if (INPLACE && (r & 3) == 3) {
+                            const uint4 v = *(const uint4*)(nrow + r - 3);
+                            P[r - 3] = v.x;
+                            P[r - 2] = v.y;
+                            P[r - 1] = v.z;
+                            P[r] = v.w;
+                        }
                         hd = H[r];
+                        const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
+                        if (AD && ((r - g0) & 1) == 0) {
+                            // H[r + 1] still holds column j-1
+                            const int ai = g0 + (r - g0 + k) % G;
+                            A[ai] = (r - g0 == G - 2) ? fmax2(h, H[r + 1]) : fmax3(A[ai], h, H[r + 1]);
+                        }
                         H[r] = h;
                         if (NW) {
                             // diagonal-relative: E and F need no extension add
@@ -644,12 +708,34 @@ pair_kernel(const StripArgs a) {
                             const uint32_t tt = h + cQ;
                             E[r] = fmax3(E[r], tt, fl[r]);
                             F = fmax2(F, tt);
-                            // x = max(H - |R|, 0) into H[r]'s slot of the S tree
-                            xs[r & 1] = psubsat16(h, fl[r]);
-                            if (r & 1) S = fmax3(S, xs[0], xs[1]);
+                            if (!AD) {
+                                // x = max(H - |R|, 0) into H[r]'s slot of the S tree
+                                xs[r & 1] = psubsat16(h, fl[r]);
+                                if (r & 1) S = fmax3(S, xs[0], xs[1]);
+                            }
+                            if (AD && r == g0) {
+                                // the group's anti-diagonal g0+j is complete:
+                                // x = max(H - |R|, 0).  One group: S takes two
+                                // columns' x per max3; several: two groups'.
+                                const uint32_t x = psubsat16(A[g0 + k % G], fl[g0]);
+                                const int gi = ad_index(r, NPS);
+                                if (NG == 1) {
+                                    xa[k & 1] = x;
+                                    if (k & 1) S = fmax3(S, xa[0], xa[1]);
+                                } else if (gi & 1) {
+                                    S = fmax3(S, xa[0], x);
+                                } else if (gi == NG - 1) {
+                                    S = fmax2(S, x);
+                                } else {
+                                    xa[0] = x;
+                                }
+                            }
+                            // row r's floor for the next column, updated in
+                            // place right after its last use (SGPRs are tight)
+                            if (FL_INROW) fl[r] += cRabs;
                         }
                     }
-                    if (!NW) {
+                    if (!NW && !FL_INROW) {
 #pragma unroll
                         for (int r = 0; r < NPS; r++) fl[r] += cRabs;
                     }
@@ -677,6 +763,22 @@ pair_kernel(const StripArgs a) {
         }
         ob[3] = FL;
         if (keep) rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        if (AD) {
+            // drain after the last column J = ncols-1: the odd local rows'
+            // cells of column J, and each group's anti-diagonals J+1 ..
+            // J+G-1 (partial).  fl[] now hold column J+1's floors; register
+            // g+p holds the group's anti-diagonal J+1+d, d = (p - ncols) mod G,
+            // floor fl[g] + d|R| (d = G-1 is anti-diagonal J, already
+            // flushed: skipped).
+#pragma unroll
+            for (int r = 0; r < NPS; r++) {
+                const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
+                if ((r - g0) & 1) S = fmax2(S, psubsat16(H[r], fl[r] - cRabs));
+                const uint32_t d = ((uint32_t)(r - g0) - gd.ncols) & (G - 1);
+                const uint32_t f = d == (uint32_t)G - 1 ? 0xffffffffu : fl[g0] + d * cRabs;
+                S = fmax2(S, psubsat16(A[r], __builtin_amdgcn_readfirstlane(f)));
+            }
+        }
     };
 
     using MainNP = std::integral_constant<int, NP>;
@@ -968,8 +1070,9 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const uint32_t blocks = (a.ngroups + kPairWaves - 1) / kPairWaves;
-    hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * kPairWaves), lds_bytes, st, a);
+    constexpr int W = pair_waves(NP, NW);
+    const uint32_t blocks = (a.ngroups + W - 1) / W;
+    hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }
 

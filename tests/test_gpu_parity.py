@@ -114,7 +114,8 @@ def test_random_golden_full_score_vectors(fname):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 2, 8, 9, 15, 16, 17, 24, 25, 31, 32, 33, 40, 41, 47, 48, 49, 63, 64, 65, 80, 81, 88, 89, 96, 97, 100])
+@pytest.mark.parametrize("qlen", [1, 2, 8, 9, 15, 16, 17, 24, 25, 31, 32, 33, 40, 41, 47, 48, 49, 63, 64, 65, 72, 73,
+                                  80, 81, 88, 89, 90, 95, 96, 97, 100, 113, 121])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_query_length_edges_vs_oracle(qlen, algo):
     rng = np.random.default_rng(qlen)
