@@ -44,7 +44,9 @@ void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
-    dfree(d_work);
+    dfree(d_work); dfree(d_top);
+    d_top = nullptr;
+    top_cap = 0;
     dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
     if (h_fbuf) (void)hipHostFree(h_fbuf);
     if (h_up) (void)hipHostFree(h_up);
@@ -783,22 +785,51 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             D.work_cap = (size_t)wide_threads * 2 * m;
         }
         hipStream_t st = D.stream;
+        // pair kernel: the first strip's top boundary (H(-1,j), F into row
+        // 0), diagonal-relative patterns, one dword per column up to the
+        // longest group's ncols (kernels.h StripArgs::top)
+        std::vector<uint32_t> top;
+        if (use_pair) {
+            const size_t ncols_max = ((size_t)(D.len_sorted.empty() ? 0 : D.len_sorted.back()) + 1 + 3) & ~(size_t)3;
+            top.resize(std::max<size_t>(ncols_max, 4));
+            if (nw) {
+                auto pat = [&](int v) { return (uint32_t)(v + (int)nw_base) & 0xffffu; };
+                std::fill(top.begin(), top.end(), pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16));
+            } else {
+                // 32-bit wrapping, exactly the kernel's combined adds
+                const uint32_t rabs = (uint32_t)(-R);
+                uint32_t v = (((uint32_t)(kF16Floor - (int)rabs)) & 0xffffu) * 0x10001u;
+                for (auto& t : top) {
+                    t = v;
+                    v += rabs * 0x10001u;
+                }
+            }
+        }
+        if (D.top_cap < top.size()) {
+            dfree(D.d_top);
+            check(hipMalloc((void**)&D.d_top, top.size() * 4), "top boundary");
+            D.top_cap = top.size();
+        }
         // one pinned staging buffer for the per-search uploads (pageable
         // sources would make each copy a synchronous staged transfer)
-        const size_t up_bytes = qpt.size() * 4 + 1024 * 8 + ((m + 15) & ~(size_t)15);
+        const size_t up_bytes = qpt.size() * 4 + top.size() * 4 + 1024 * 8 + ((m + 15) & ~(size_t)15);
         if (D.h_up_cap < up_bytes) {
             if (D.h_up) (void)hipHostFree(D.h_up);
             check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
             D.h_up_cap = up_bytes;
         }
         uint8_t* up_q = D.h_up;
-        uint8_t* up_m = up_q + qpt.size() * 4;
+        uint8_t* up_t = up_q + qpt.size() * 4;
+        uint8_t* up_m = up_t + top.size() * 4;
         uint8_t* up_s = up_m + 1024 * 8;
         memcpy(up_q, qpt.data(), qpt.size() * 4);
+        if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_m, Mc, 1024 * 8);
         memcpy(up_s, qv.seq, m);
         check(hipEventRecord(D.ev[4], st), "event");
         check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+        if (!top.empty())
+            check(hipMemcpyAsync(D.d_top, up_t, top.size() * 4, hipMemcpyHostToDevice, st), "H2D top");
         check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
         check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
         check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
@@ -849,6 +880,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             StripArgs b = a;
             b.nstrips = main_strips;
             b.qpt_tail = D.d_qpt + tail_off;
+            b.top = (const uint4*)D.d_top;
             const int lnp = main_strips ? pnp : tail_np;
             check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {

@@ -56,6 +56,8 @@ struct DeviceDB {
     int64_t* h_wide = nullptr;            // pinned
     uint32_t* d_qpt = nullptr;
     size_t qpt_cap = 0;
+    uint32_t* d_top = nullptr;            // pair_kernel first-strip boundary quads
+    size_t top_cap = 0;
     uint8_t* d_query = nullptr;
     size_t query_cap = 0;
     int64_t* d_matrix = nullptr;

@@ -34,6 +34,10 @@ struct StripArgs {
     uint32_t nw_base;          // NW pattern offset of pair_kernel (value + nw_base)
     // pair_kernel: the tail strip's table (launch_pair's npt > 0)
     const uint32_t* qpt_tail;
+    // pair_kernel: top boundary of the first strip, (H(-1,j), F into row 0)
+    // as diagonal-relative patterns in row-buffer quads, the same for every
+    // lane ([ceil(max ncols / 4)] uint4)
+    const uint4* top;
 };
 
 struct WideArgs {

@@ -593,8 +593,11 @@ pair_kernel(const StripArgs a) {
         uint32_t hd0 = NW ? pat(first ? 2 * R : Q + 2 * R) | (pat(Q + 4 * R) << 16)
                           : pat((i0 - 2) * (int)Rabs) | (pat(0) << 16);
         uint32_t Fprev = 0x0400u;
-        // synthesized top boundary of the first strip: (H(-1,j), F into row 0)
-        uint32_t rbsyn = NW ? (pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16)) : pat(-(int)Rabs) * 0x10001u;
+        // the boundary row above the strip: the previous strip's row buffer,
+        // or for the first strip the lane-independent top boundary a.top
+        // (a broadcast read; no per-column select between the two)
+        const uint4* qsrc = first ? a.top : rbp;
+        const uint32_t qstride = first ? 1 : 64;
 
         // SW, anti-diagonal maxima (AD): cells (r, j) and (r+1, j-1) have the
         // same diagonal-relative offset i0+r+j, so the running maximum needs no
@@ -625,7 +628,7 @@ pair_kernel(const StripArgs a) {
         uint4 qn[PF];
 #pragma unroll
         for (int p = 0; p < PF; p++)
-            qn[p] = (first || (uint32_t)p >= nquads) ? make_uint4(0, 0, 0, 0) : rbp[(size_t)p * 64];
+            qn[p] = (uint32_t)p >= nquads ? make_uint4(0, 0, 0, 0) : qsrc[(size_t)p * qstride];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
         uint32_t dprev = a.alpha;
         // P: the current column's profile operands.  INPLACE: the next
@@ -650,9 +653,9 @@ pair_kernel(const StripArgs a) {
                 const uint4 qcur = qn[0];
 #pragma unroll
                 for (int p = 0; p + 1 < PF; p++) qn[p] = qn[p + 1];
-                if (!first) {
+                {
                     const uint32_t nq = b * 4 + t + PF;
-                    if (nq < nquads) qn[PF - 1] = rbp[(size_t)nq * 64];
+                    if (nq < nquads) qn[PF - 1] = qsrc[(size_t)nq * qstride];
                 }
                 const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
 #pragma unroll
@@ -671,13 +674,7 @@ pair_kernel(const StripArgs a) {
                         for (int r = 0; r < NPS; r++) P[r] = nxt[r];
                         load_row<NPS>(nxt, nrow);
                     }
-                    uint32_t rbv;
-                    if (first) {
-                        rbv = rbsyn;
-                        if (!NW) rbsyn += cRabs;
-                    } else {
-                        rbv = qw[u];
-                    }
+                    const uint32_t rbv = qw[u];
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
                     uint32_t xs[2];
