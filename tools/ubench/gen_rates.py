@@ -50,7 +50,16 @@ INSTRS = {
     "mix_pkadd_max3": "v_pk_add_u16 %0, %0, %1\\n\\tv_pk_maximum3_f16 %0, %0, %1, %2",
     "v_pk_maximum3_f16x2": "v_pk_maximum3_f16 %0, %0, %1, %2\\n\\tv_pk_maximum3_f16 %0, %0, %2, %1",
     "v_add_u32x2": "v_add_u32 %0, %0, %1\\n\\tv_add_u32 %0, %0, %2",
+    "v_mul_lo_u32": "v_mul_lo_u32 %0, %0, %1",
+    "v_mul_hi_u32": "v_mul_hi_u32 %0, %0, %1",
+    "v_mad_u32_u24": "v_mad_u32_u24 %0, %0, %1, %2",
+    "v_mul_u32_u24": "v_mul_u32_u24 %0, %0, %1",
+    "v_bfe_u32": "v_bfe_u32 %0, %0, 8, 8",
+    "v_lshrrev_b32": "v_lshrrev_b32 %0, 8, %0",
+    "v_and_or_b32": "v_and_or_b32 %0, %0, %1, %2",
+    "v_lshl_or_b32": "v_lshl_or_b32 %0, %0, 4, %1",
 }
+import os
 import sys
 only = sys.argv[1:] if len(sys.argv) > 1 else list(INSTRS)
 src = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdint>']
@@ -93,4 +102,4 @@ int main() {''')
 for name in only:
     src.append(f'    run("{name}", k_{name});')
 src.append('    return 0;\n}')
-open('valu_rates2.hip', 'w').write('\n'.join(src) + '\n')
+open(os.environ.get('OUT', 'valu_rates2.hip'), 'w').write('\n'.join(src) + '\n')
