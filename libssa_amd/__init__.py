@@ -209,14 +209,28 @@ def stats():
     return d
 
 
+_hitbuf = [None, 0]     # reused output array (a fresh 64 Ki-entry ctypes array per call costs ~0.2 ms)
+
+
+def _hits(cap):
+    if _hitbuf[1] < cap:
+        _hitbuf[0], _hitbuf[1] = (ssa_hit_t * cap)(), cap
+    return _hitbuf[0]
+
+
 def search(q, algo, hitcount, bit_width=BIT_WIDTH_16, mode=TOPK, cap=None):
     """ssa_amd_search: sorted top-k (mode=TOPK) or the shard insertion log
     (mode=LOG) as a list of (score, global_id, query_id, strand, frame)."""
     L = load()
+    explicit = cap is not None
     if cap is None:
         cap = max(hitcount, 1) if mode == TOPK else max(4 * hitcount + 4096, 65536)
-    buf = (ssa_hit_t * cap)()
-    n = L.ssa_amd_search(q, algo, hitcount, bit_width, mode, buf, cap)
+    while True:
+        buf = _hits(cap)
+        n = L.ssa_amd_search(q, algo, hitcount, bit_width, mode, buf, cap)
+        if n < cap or explicit or mode == TOPK:
+            break
+        cap *= 4            # a log filled the buffer: search again with room
     return [(buf[i].score, buf[i].db_id, buf[i].query_id, buf[i].db_strand, buf[i].db_frame) for i in range(n)]
 
 

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cuts, k, outdir):
+def _worker(rank, world, port, cuts, k, outdir, cap=None):
     import torch.distributed as dist
     import libssa_amd as S
     from libssa_amd.dist import global_topk
@@ -43,12 +43,13 @@ def _worker(rank, world, port, cuts, k, outdir):
     lens = np.diff(off)[a:b]
     keep = np.nonzero(lens > 0)[0]
     log = po.topk_log(sc[keep], (keep + a).astype(np.uint64), k)
-    res = global_topk([(s, i, 0, 0, 0) for s, i in log], k, dist, rank, world, "cpu")
+    res = global_topk([(s, i, 0, 0, 0) for s, i in log], k, dist, rank, world, "cpu",
+                      **({} if cap is None else {"cap": cap}))
     if rank == 0:
         allsc = po.scores(0, q, codes, off, M, -11, -1)
         nz = np.nonzero(np.diff(off) > 0)[0]
         exp = po.topk(allsc[nz], nz.astype(np.uint64), k)
-        with open(os.path.join(outdir, f"r{k}.txt"), "w") as f:
+        with open(os.path.join(outdir, f"r{k}_{cap}.txt"), "w") as f:
             f.write("ok" if res == exp else f"mismatch {res[:5]} {exp[:5]}")
     dist.destroy_process_group()
 
@@ -57,7 +58,15 @@ def _worker(rank, world, port, cuts, k, outdir):
 @pytest.mark.parametrize("k", [1, 10, 137])
 def test_gloo_gather_replay_equals_single_process(tmp_path, world, cuts, k):
     mp.spawn(_worker, args=(world, _free_port(), cuts, k, str(tmp_path)), nprocs=world, join=True)
-    assert open(tmp_path / f"r{k}.txt").read() == "ok"
+    assert open(tmp_path / f"r{k}_None.txt").read() == "ok"
+
+
+@pytest.mark.parametrize("cap", [1, 40])
+def test_gloo_log_longer_than_cap_falls_back(tmp_path, cap):
+    """A shard log longer than the fixed exchange buffer takes the exact-size
+    gather; the result is unchanged."""
+    mp.spawn(_worker, args=(2, _free_port(), [0, 1500, 3000], 137, str(tmp_path), cap), nprocs=2, join=True)
+    assert open(tmp_path / f"r137_{cap}.txt").read() == "ok"
 
 
 def test_shard_log_property():
