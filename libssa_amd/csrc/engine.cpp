@@ -709,8 +709,9 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
         // rows up to the last strip's end so table builders need no bounds test
         const size_t mpad = std::max<size_t>((size_t)nstrips * 2 * np, m + 2 * pnp) + 64;
-        std::vector<uint16_t> P((size_t)(A + 1) * mpad, (uint16_t)padv);
-        for (uint32_t c = 0; c < A; c++) {
+        // (the pair kernel's tables are built on the device: pair_tables_kernel)
+        std::vector<uint16_t> P(use_pair ? 0 : (size_t)(A + 1) * mpad, (uint16_t)padv);
+        for (uint32_t c = 0; c < (use_pair ? 0u : A); c++) {
             const int64_t* row = M + ((size_t)D.code_of[c] << 5);
             uint16_t* pc = P.data() + (size_t)c * mpad;
             for (size_t i = 0; i < m; i++)
@@ -722,6 +723,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // tail strip of the smallest height (multiple of 8 rows) that holds the
         // remainder; NW always ends in a tail strip, which captures its score
         std::vector<uint32_t> qpt;
+        size_t qpt_words = 0;                // device table size (dwords)
         uint32_t main_strips = 0;
         int tail_np = 0;
         size_t tail_off = 0;
@@ -735,27 +737,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 full--;
                 tail_np = pnp;
             }
-            auto add_tables = [&](int Ph, uint32_t row0, uint32_t count) {
-                const size_t off = qpt.size();
-                qpt.resize(off + (size_t)count * prow * prow * Ph);
-                uint32_t* dst = qpt.data() + off;
-                for (uint32_t s = 0; s < count; s++) {
-                    const size_t i0 = row0 + (size_t)s * 2 * Ph;
-                    for (uint32_t c1 = 0; c1 < prow; c1++) {
-                        const uint16_t* lo = prow_of(c1) + i0;
-                        for (uint32_t c0 = 0; c0 < prow; c0++) {
-                            const uint16_t* hi = prow_of(c0) + i0 + Ph;
-                            for (int r = 0; r < Ph; r++) *dst++ = (uint32_t)lo[r] | ((uint32_t)hi[r] << 16);
-                        }
-                    }
-                }
-                return off;
-            };
             main_strips = full;
-            add_tables(pnp, 0, full);
-            if (tail_np) tail_off = add_tables(tail_np, full * Hm, 1);
+            tail_off = (size_t)full * prow * prow * pnp;
+            qpt_words = tail_off + (size_t)prow * prow * tail_np;
         } else {
             qpt.resize((size_t)nstrips * 32 * np);
+            qpt_words = qpt.size();
             for (uint32_t s = 0; s < nstrips; s++)
                 for (uint32_t c = 0; c < 32; c++)
                     for (int r = 0; r < np; r++) {
@@ -768,10 +755,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         int64_t Mc[1024];
         for (int x = 0; x < 32; x++)
             for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(D.code_of[x] << 5) + y] : -1;
-        if (D.qpt_cap < qpt.size()) {
+        if (D.qpt_cap < qpt_words) {
             dfree(D.d_qpt);
-            check(hipMalloc((void**)&D.d_qpt, qpt.size() * 4), "qpt");
-            D.qpt_cap = qpt.size();
+            check(hipMalloc((void**)&D.d_qpt, qpt_words * 4), "qpt");
+            D.qpt_cap = qpt_words;
         }
         if (D.query_cap < m) {
             dfree(D.d_query);
@@ -822,16 +809,32 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         uint8_t* up_t = up_q + qpt.size() * 4;
         uint8_t* up_m = up_t + top.size() * 4;
         uint8_t* up_s = up_m + 1024 * 8;
-        memcpy(up_q, qpt.data(), qpt.size() * 4);
+        if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
         if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_m, Mc, 1024 * 8);
         memcpy(up_s, qv.seq, m);
         check(hipEventRecord(D.ev[4], st), "event");
-        check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+        if (!qpt.empty())
+            check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
         if (!top.empty())
             check(hipMemcpyAsync(D.d_top, up_t, top.size() * 4, hipMemcpyHostToDevice, st), "H2D top");
         check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
         check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        if (use_pair) {
+            TableArgs ta{};
+            ta.query = D.d_query;
+            ta.matrix = D.d_matrix;
+            ta.out = D.d_qpt;
+            ta.m = (uint32_t)m;
+            ta.alpha = A;
+            ta.np = (uint32_t)pnp;
+            ta.nmain = main_strips;
+            ta.npt = (uint32_t)tail_np;
+            ta.tail_row0 = main_strips * 2 * (uint32_t)pnp;
+            ta.rel = rel;
+            ta.pad = (uint32_t)(uint16_t)padv;
+            check(launch_pair_tables(ta, st), "pair tables kernel");
+        }
         check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
 
         StripArgs a{};
@@ -983,7 +986,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         dms += t;
         if (trace_on()) fprintf(stderr, "trace: post-sync %.3f\n", now_ms() - t_post0);
         // algorithmic bytes: residues once + per-entry score write + profile
-        kernel_bytes += D.meta.residues + 4ull * E + qpt.size() * 4;
+        kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
     }
     if (trace_on())
         fprintf(stderr, "trace: prep %.3f sync %.3f total %.3f\n", prep, sync_wait, now_ms() - t_prep0);

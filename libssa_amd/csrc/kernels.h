@@ -84,4 +84,21 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 
+// pair_kernel's per-search pair tables, built on the device from the query
+// and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)
+// then the tail strip ((alpha+1)^2 x npt dwords).  Dword (c1*(alpha+1)+c0, r)
+// of a strip from row i0 = (P(c1, i0+r), P(c0, i0+np+r)), P(c, i) =
+// clamp16(M[c][q_i] + rel) for a real code and row, pad otherwise.
+struct TableArgs {
+    const uint8_t* query;      // [m] query codes
+    const int64_t* matrix;     // [1024] compact-code matrix (x = DB code)
+    uint32_t* out;             // main tables, then the tail table
+    uint32_t m, alpha;
+    uint32_t np, nmain;        // main strip half-height and count
+    uint32_t npt, tail_row0;   // tail strip half-height (0: none) and first row
+    int32_t rel;               // added to every real profile value (-2R)
+    uint32_t pad;              // 16-bit padding value
+};
+hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
+
 }  // namespace ssa

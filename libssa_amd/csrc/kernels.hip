@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "kernels.h"
@@ -1031,6 +1032,46 @@ hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(filter_block, dim3(a.nblocks), dim3(256), 0, st, a);
     hipLaunchKernelGGL(filter_prefix, dim3(1), dim3(64 * kPrefixWaves), 0, st, a);
     hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// Per-search pair tables for pair_kernel (kernels.h TableArgs): one thread
+// per dword, replacing a host build + a ~400 KB upload per search.
+__device__ __forceinline__ uint32_t table_val(const TableArgs& a, uint32_t c, uint32_t i) {
+    if (c >= a.alpha || i >= a.m) return a.pad;
+    int64_t v = a.matrix[(c << 5) + a.query[i]] + a.rel;
+    v = v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+    return (uint32_t)(uint16_t)(int16_t)v;
+}
+
+__global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
+    const uint32_t prow = a.alpha + 1;
+    const uint32_t per_main = prow * prow * a.np;
+    const uint32_t nmain = a.nmain * per_main;
+    const uint32_t total = nmain + prow * prow * a.npt;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        uint32_t ph, i0, rem;
+        if (t < nmain) {
+            ph = a.np;
+            i0 = (t / per_main) * 2 * a.np;
+            rem = t % per_main;
+        } else {
+            ph = a.npt;
+            i0 = a.tail_row0;
+            rem = t - nmain;
+        }
+        const uint32_t pair = rem / ph, r = rem % ph;
+        const uint32_t c1 = pair / prow, c0 = pair % prow;
+        a.out[t] = table_val(a, c1, i0 + r) | (table_val(a, c0, i0 + ph + r) << 16);
+    }
+}
+
+hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
+    const uint32_t prow = a.alpha + 1;
+    const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);
+    if (total == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(pair_tables_kernel, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
