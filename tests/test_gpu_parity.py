@@ -663,3 +663,27 @@ def test_search_batch_matches_single_queries():
                 assert S.search_batch(qs, algo, k) == [[(h["score"], h["id"]) for h in fn(q, k, 16)] for q in qs]
         for q in qs:
             S.free_sequence(q)
+
+
+CLI = os.path.join(os.path.dirname(po.__file__), "_ref", "libssa_example_amd")
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="reference CLI not built (make -C oracle ref)")
+@pytest.mark.parametrize("algo", ["SW", "NW"])
+@pytest.mark.parametrize("bits", [8, 16, 64])
+def test_reference_cli_links_and_matches(algo, bits):
+    """The reference's own caller, src/libssa_example.c, compiled unchanged
+    against include/libssa.h and linked to libssa_amd.so (oracle/Makefile),
+    searches on the GPU and prints the reference's 64-bit top-300 list for
+    the C1-style query (Q3ZAI3, BLOSUM62, gaps -11/-1, AF091148 as protein)."""
+    import re
+    import subprocess
+    case = next(c for c in KATS if c["name"] == "config1_Q3ZAI3_k300")
+    r = subprocess.run([CLI, "-N", "4", "-O", "-11", "-E", "-1", "-M", "BLOSUM62", "-i", os.path.join(DATA, "Q3ZAI3.fasta"),
+                        "-d", os.path.join(DATA, case["db"]), "-c", "300", "-t", algo, "-b", str(bits), "-s", "AVX2"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Nr of alignments: 300" in r.stdout
+    line = r.stdout.split("(Score, DB-ID), ")[1].splitlines()[0]
+    got = [(int(a), int(b)) for a, b in re.findall(r"\((-?\d+), (\d+)\)", line)]
+    assert got == [tuple(x) for x in case[algo.lower() + "_64"]]
