@@ -203,3 +203,27 @@ def test_packed_db_refuses_foreign_files(tmp_path):
     other.write_bytes(hdr)
     assert S.load_db(str(other)) != 0
     S.set_output_mode(S.OUTPUT_WARNING)
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "benchmark", "src")), reason="reference tree absent")
+@pytest.mark.parametrize("main", ["src/libssa_example.c", "benchmark/src/benchmark_base_test_run.c",
+                                  "benchmark/src/benchmark_chunks.c", "benchmark/src/benchmark_pairwise.c",
+                                  "benchmark/src/benchmark_queries.c", "benchmark/src/benchmark_threads.c"])
+def test_reference_callers_compile_and_link_unchanged(tmp_path, main):
+    """SURVEY §8b "callers to keep linking": the reference's own CLI and
+    benchmark drivers, compiled from their sources where they lie (never
+    copied) and linked against libssa_amd.so with every symbol resolved.
+    (The benchmark drivers include ../../src/libssa.h, the reference's
+    header, whose ABI include/libssa.h reproduces.)"""
+    srcs = [os.path.join(REF, main)]
+    if main.startswith("benchmark/"):
+        srcs.append(os.path.join(REF, "benchmark", "src", "benchmark_util.c"))
+    exe = tmp_path / "caller"
+    r = subprocess.run(["gcc", "-std=gnu99", "-w", "-I", os.path.join(ROOT, "include"), *srcs, "-o", str(exe),
+                        "-L", S.LIB_DIR, "-lssa_amd", "-lssa_fasta_db", f"-Wl,-rpath,{S.LIB_DIR}",
+                        "-Wl,--no-undefined"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert exe.exists()
