@@ -12,7 +12,7 @@ from __future__ import annotations
 # rows per rank of the single fixed-size exchange; a shard log is a few
 # dozen to a few hundred entries (k * (1 + ln(shard / k)) expected), longer
 # ones take the two-step variable-size path
-LOG_CAP = 2048
+LOG_CAP = 512
 
 
 def _rows(log):

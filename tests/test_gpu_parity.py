@@ -687,3 +687,29 @@ def test_reference_cli_links_and_matches(algo, bits):
     line = r.stdout.split("(Score, DB-ID), ")[1].splitlines()[0]
     got = [(int(a), int(b)) for a, b in re.findall(r"\((-?\d+), (\d+)\)", line)]
     assert got == [tuple(x) for x in case[algo.lower() + "_64"]]
+
+
+@pytest.mark.parametrize("gaps", [(0, 0), (-5, 0), (0, -1), (-1, -3), (-20, -7)])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_gap_penalty_edges_vs_oracle(gaps, algo):
+    """Zero gap-open/extension and steep gaps: the diagonal-relative frame's
+    offsets and floors (|R| = 0 makes every floor equal) stay exact."""
+    rng = np.random.default_rng(5)
+    q = syn.protein_query(57, 11)
+    lens = np.array([0, 1, 5, 17, 48, 49, 130] + list(rng.integers(1, 200, 150)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp = po.scores(algo, q, codes, off, M, gaps[0], gaps[1])[keep]
+    configure(False, ("builtin", "blosum62"), gaps[0], gaps[1])
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for pnp in (16, 24):
+            S.set_option("pair_np", pnp)
+            sc, ids = _full_scores(qq, algo, len(keep))
+            assert (sc == exp).all(), (pnp, np.nonzero(sc != exp)[0][:10])
+        S.set_option("pair_np", 24)
+        S.free_sequence(qq)
