@@ -42,9 +42,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # (NW) searches: profiles/r01/pmc_c2_sw_np16 (strip16), pmc_c2_r01b and
 # pmc_c3_r01b (32-row pair strips), pmc_c2_np24 / pmc_c3_np24 (48-row strips),
 # pmc_c2_rel / pmc_c3_rel (48-row strips, diagonal-relative values),
-# pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals: the
+# pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals),
+# pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory: the
 # default, these values)
-VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 3.11, "pair_f16_nw": 2.79}
+VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 3.05, "pair_f16_nw": 2.74}
 
 
 def parse():
@@ -249,7 +250,7 @@ def main():
     # VALU issue roofline: the strip kernel is made of
     # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
     # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
-    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01d).
+    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01e).
     instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 and args.pair_np == 24 else None
     issue_cycles = 4.17
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None

@@ -632,15 +632,13 @@ pair_kernel(const StripArgs a) {
             qn[p] = (uint32_t)p >= nquads ? make_uint4(0, 0, 0, 0) : qsrc[(size_t)p * qstride];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
         uint32_t dprev = a.alpha;
-        // P: the current column's profile operands.  INPLACE: the next
-        // column's row is loaded into P behind the row loop, four rows at a
-        // time (no second buffer: the registers pay for AD's accumulators)
-        constexpr bool INPLACE = true;
+        // P: the current column's profile operands.  The next column's row
+        // is loaded into P in place behind the row loop, four rows at a time
+        // (no second buffer: the registers pay for the SW accumulators A)
         uint32_t P[NPS];
-        uint32_t nxt[NPS];   // unused when INPLACE
         {
             const uint32_t d0 = rnext.x & 0xffu;
-            load_row<NPS>(INPLACE ? P : nxt, lds + (d0 * prow + dprev) * ROWW);
+            load_row<NPS>(P, lds + (d0 * prow + dprev) * ROWW);
             dprev = d0;
         }
 
@@ -670,11 +668,6 @@ pair_kernel(const StripArgs a) {
                         nrow = lds + (dn * prow + dprev) * ROWW;
                         dprev = dn;
                     }
-                    if constexpr (!INPLACE) {
-#pragma unroll
-                        for (int r = 0; r < NPS; r++) P[r] = nxt[r];
-                        load_row<NPS>(nxt, nrow);
-                    }
                     const uint32_t rbv = qw[u];
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
@@ -682,7 +675,7 @@ pair_kernel(const StripArgs a) {
 #pragma unroll
                     for (int r = 0; r < NPS; r++) {
                         const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
-                        if (INPLACE && (r & 3) == 3) {
+                        if ((r & 3) == 3) {
                             const uint4 v = *(const uint4*)(nrow + r - 3);
                             P[r - 3] = v.x;
                             P[r - 2] = v.y;
