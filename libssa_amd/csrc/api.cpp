@@ -51,7 +51,8 @@ void replay(const SearchScores& sc, const EntryMeta& meta, const std::vector<Que
     };
     (void)views;
     if (sc.sparse) {
-        for (const uint32_t e : sc.cand) visit(0, e);
+        // candidates in insertion order, as view * entries + entry
+        for (const uint32_t x : sc.cand) visit(x / E, x % E);
         return;
     }
     if (V == 1) {

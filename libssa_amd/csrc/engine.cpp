@@ -44,7 +44,13 @@ void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
-    dfree(d_work); dfree(d_top);
+    dfree(d_work); dfree(d_top); dfree(d_order);
+    d_order = nullptr;
+    h_order.clear();
+    order_key = ~0ull;
+    scores_cap = filter_cap = 0;
+    for (auto& e : vev) (void)hipEventDestroy(e);
+    vev.clear();
     d_top = nullptr;
     top_cap = 0;
     dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
@@ -321,15 +327,17 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     dalloc((void**)&D.d_lane_out, H.lane_out.size() * 4, "lane_out");
     {
         const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
-        dalloc((void**)&D.d_fbuf, 16 + std::max<size_t>(E, 1) * 8, "filter candidates");
+        dalloc((void**)&D.d_fbuf, kFilterHeader * 4 + std::max<size_t>(E, 1) * 8, "filter candidates");
+        D.filter_cap = std::max<size_t>(E, 1);
         dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
         dalloc((void**)&D.d_before, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter scan");
         dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
         dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
         D.h_cand_cap = 4096;
-        check(hipHostMalloc((void**)&D.h_fbuf, 16 + D.h_cand_cap * 8, hipHostMallocDefault), "pinned");
+        check(hipHostMalloc((void**)&D.h_fbuf, kFilterHeader * 4 + D.h_cand_cap * 8, hipHostMallocDefault), "pinned");
     }
     dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
+    D.scores_cap = std::max<size_t>(E, 1);
     dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
     dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
     dalloc((void**)&D.d_matrix, 1024 * 8, "matrix");
@@ -641,7 +649,59 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     const double t_prep0 = now_ms();
     double prep = 0, sync_wait = 0;
     float upload = 0;
-    out.sparse = V == 1 && k > 0 && k <= (size_t)kFilterMaxK && E > 0 && views[0].len > 0 && !cfg().no_filter;
+    bool all_rows = V > 0;
+    for (const auto& qv : views) all_rows = all_rows && qv.len > 0;
+    out.sparse = V <= (size_t)kFilterMaxViews && k > 0 && k <= (size_t)kFilterMaxK && E > 0 && all_rows &&
+                 !cfg().no_filter;
+    // several views: enqueued back to back (host preparation of view v+1
+    // overlaps view v on the GPU), each into its own score and overflow
+    // slice, then one filter pass over all (view, entry) scores in the
+    // reference's chunk-interleaved insertion order -- no per-view sync,
+    // copy or host scan of every score
+    const bool multi = out.sparse && V > 1;
+    const size_t ovf_capv = multi ? kOvfCap / V - 1 : kOvfCap;
+    if (multi) {
+        if (D.scores_cap < V * E) {
+            dfree(D.d_scores);
+            check(hipMalloc((void**)&D.d_scores, V * E * 4), "scores");
+            D.scores_cap = V * E;
+        }
+        if (D.filter_cap < V * E) {
+            const size_t nb = (V * E + kFilterBlock - 1) / kFilterBlock;
+            dfree(D.d_fbuf); dfree(D.d_summary); dfree(D.d_before); dfree(D.d_thresh_local); dfree(D.d_thresh);
+            check(hipMalloc((void**)&D.d_fbuf, kFilterHeader * 4 + V * E * 8), "filter candidates");
+            check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 4), "filter summaries");
+            check(hipMalloc((void**)&D.d_before, nb * kFilterMaxK * 4), "filter scan");
+            check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
+            check(hipMalloc((void**)&D.d_thresh, nb * 4), "filter thresholds");
+            D.filter_cap = V * E;
+        }
+        // insertion order (replay() in api.cpp): ID chunks of chunk_size,
+        // views outer inside a chunk, entries in ID order
+        const uint64_t cs = C.chunk_size;
+        const uint64_t key = (uint64_t)V << 48 ^ cs << 20 ^ E;
+        if (D.order_key != key) {
+            D.h_order.resize(V * E);
+            size_t p = 0, e0 = 0;
+            while (e0 < E) {
+                const uint64_t chunk_end = (D.meta.id[e0] / cs + 1) * cs;
+                size_t e1 = e0;
+                while (e1 < E && D.meta.id[e1] < chunk_end) e1++;
+                for (size_t v = 0; v < V; v++)
+                    for (size_t e = e0; e < e1; e++) D.h_order[p++] = (uint32_t)(v * E + e);
+                e0 = e1;
+            }
+            dfree(D.d_order);
+            check(hipMalloc((void**)&D.d_order, V * E * 4), "insertion order");
+            check(hipMemcpy(D.d_order, D.h_order.data(), V * E * 4, hipMemcpyHostToDevice), "H2D order");
+            D.order_key = key;
+        }
+        while (D.vev.size() < 2 * V) {
+            hipEvent_t e;
+            check(hipEventCreate(&e), "hipEventCreate");
+            D.vev.push_back(e);
+        }
+    }
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
     uint64_t kernel_bytes = 0;
@@ -805,6 +865,9 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
             D.h_up_cap = up_bytes;
         }
+        // the staging buffer is reused: in a multi-view search the previous
+        // view's copies may still be queued behind its predecessor's kernel
+        if (multi && v > 0) check(hipEventSynchronize(D.ev[5]), "staging");
         uint8_t* up_q = D.h_up;
         uint8_t* up_t = up_q + qpt.size() * 4;
         uint8_t* up_m = up_t + top.size() * 4;
@@ -820,6 +883,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMemcpyAsync(D.d_top, up_t, top.size() * 4, hipMemcpyHostToDevice, st), "H2D top");
         check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
         check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        if (multi) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
         if (use_pair) {
             TableArgs ta{};
             ta.query = D.d_query;
@@ -835,7 +899,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.pad = (uint32_t)(uint16_t)padv;
             check(launch_pair_tables(ta, st), "pair tables kernel");
         }
-        check(hipMemsetAsync(D.d_ovf, 0, 4, st), "memset");
+        // overflow list of this view: the whole list, or in a multi-view
+        // search its own slice (all views stay on the device until the end)
+        uint32_t* ovf = D.d_ovf + (multi ? v * (ovf_capv + 1) : 0);
+        int64_t* wide = D.d_wide + (multi ? v * ovf_capv : 0);
+        check(hipMemsetAsync(ovf, 0, 4, st), "memset");
 
         StripArgs a{};
         a.res = D.d_res;
@@ -844,16 +912,16 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         a.lane_len = D.d_lane_len;
         a.lane_out = D.d_lane_out;
         a.qpt = D.d_qpt;
-        a.scores = D.d_scores;
-        a.ovf_list = D.d_ovf + 1;
-        a.ovf_count = D.d_ovf;
+        a.scores = D.d_scores + (multi ? v * E : 0);
+        a.ovf_list = ovf + 1;
+        a.ovf_count = ovf;
         a.ngroups = D.ngroups;
         a.nstrips = nstrips;
         a.m = (uint32_t)m;
         a.gap_open = Q;
         a.gap_extend = R;
         a.nmax16 = nmax16;
-        a.ovf_cap = (uint32_t)kOvfCap;
+        a.ovf_cap = (uint32_t)ovf_capv;
         a.pad_word = (uint32_t)(uint16_t)padv * 0x10001u;
         a.alpha = A;
         a.nw_base = nw_base;
@@ -862,23 +930,24 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         w.res = D.d_res;
         w.groups = D.d_groups;
         w.lane_len = D.d_lane_len;
-        w.ovf_list = D.d_ovf + 1;
-        w.ovf_count = D.d_ovf;
+        w.ovf_list = ovf + 1;
+        w.ovf_count = ovf;
         w.query = D.d_query;
         w.matrix = D.d_matrix;
         w.work = D.d_work;
-        w.wide_scores = D.d_wide;
+        w.wide_scores = wide;
         w.m = (uint32_t)m;
         w.gap_open = Q;
         w.gap_extend = R;
         w.nw = nw ? 1 : 0;
-        w.ovf_cap = (uint32_t)kOvfCap;
+        w.ovf_cap = (uint32_t)ovf_capv;
 
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
         if (v == 0) prep = now_ms() - t_prep0;
-        check(hipEventRecord(D.ev[0], st), "event");
+        hipEvent_t ev_k0 = multi ? D.vev[2 * v] : D.ev[0], ev_k1 = multi ? D.vev[2 * v + 1] : D.ev[1];
+        check(hipEventRecord(ev_k0, st), "event");
         if (use_pair) {
             StripArgs b = a;
             b.nstrips = main_strips;
@@ -889,15 +958,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
-        check(hipEventRecord(D.ev[1], st), "event");
+        check(hipEventRecord(ev_k1, st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
+        kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
+        if (multi && v + 1 < V) continue;
         check(hipEventRecord(D.ev[2], st), "event");
         if (out.sparse) {
             FilterArgs f{};
             f.scores = D.d_scores;
-            f.n = (uint32_t)E;
+            f.order = multi ? D.d_order : nullptr;
+            f.n = (uint32_t)(multi ? V * E : E);
             f.k = (uint32_t)k;
-            f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
+            f.nblocks = (uint32_t)((f.n + kFilterBlock - 1) / kFilterBlock);
             f.nw = nw ? 1 : 0;
             f.bw = bw;
             f.summary = D.d_summary;
@@ -905,88 +977,90 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             f.thresh_local = D.d_thresh_local;
             f.before = D.d_before;
             f.ovf_count = D.d_ovf;
+            f.ovf_stride = (uint32_t)(ovf_capv + 1);
+            f.nviews = (uint32_t)(multi ? V : 1);
             f.counters = D.d_fbuf;
-            f.cand = (uint2*)(D.d_fbuf + 4);
-            check(hipMemsetAsync(D.d_fbuf, 0, 16, st), "memset");
+            f.cand = (uint2*)(D.d_fbuf + kFilterHeader);
+            check(hipMemsetAsync(D.d_fbuf, 0, kFilterHeader * 4, st), "memset");
             check(launch_filter(f, st), "filter launch");
-            // one copy: counters (incl. the overflow count) + the first candidates
-            const size_t first = std::min(D.h_cand_cap, E);
-            check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, 16 + 8 * first, hipMemcpyDeviceToHost, st), "D2H candidates");
+            // one copy: counters (incl. the overflow counts) + the first candidates
+            const size_t first = std::min<size_t>(D.h_cand_cap, f.n);
+            check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
+                  "D2H candidates");
         } else {
             check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
-        }
-        if (!out.sparse) {
             check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
             check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
         }
         check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
-        if (trace_on()) {
-            const double a0 = now_ms();
-            check(hipEventSynchronize(D.ev[4]), "ev");
-            const double a1 = now_ms();
-            check(hipEventSynchronize(D.ev[0]), "ev");
-            const double a2 = now_ms();
-            check(hipEventSynchronize(D.ev[1]), "ev");
-            const double a3 = now_ms();
-            fprintf(stderr, "trace: enqueue %.3f  ev4 +%.3f ev0 +%.3f ev1 +%.3f (from sync start)\n",
-                    t_sync0 - (t_prep0 + prep), a1 - a0, a2 - a0, a3 - a0);
-        }
         check(hipStreamSynchronize(st), "search");
         sync_wait += now_ms() - t_sync0;
         const double t_post0 = now_ms();
 
         {
             float u;
-            check(hipEventElapsedTime(&u, D.ev[4], D.ev[0]), "elapsed");
+            check(hipEventElapsedTime(&u, D.ev[4], ev_k0), "elapsed");
             upload += u;
         }
-        uint32_t nov;
+        // exact int64 scores of overflowed lanes: view vv's list and scores
+        auto take_wide = [&](size_t vv, uint32_t nov) {
+            if (nov > ovf_capv) fatal("overflow list exhausted (%u entries)", nov);
+            const uint32_t* ov = D.d_ovf + (multi ? vv * (ovf_capv + 1) : 0);
+            const int64_t* wd = D.d_wide + (multi ? vv * ovf_capv : 0);
+            if (out.sparse || nov > 4096) {
+                check(hipMemcpy(D.h_ovf, ov, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
+                check(hipMemcpy(D.h_wide, wd, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
+            }
+            for (uint32_t i = 0; i < nov; i++) {
+                const uint32_t e = D.lane_out[D.h_ovf[1 + i]];
+                out.wide[(uint64_t)vv * E + e] = D.h_wide[i];
+            }
+            wide_total += nov;
+        };
         if (out.sparse) {
             const uint32_t nc = D.h_fbuf[0];
-            nov = D.h_fbuf[3];
-            const uint2* cand = (const uint2*)(D.h_fbuf + 4);
+            const uint2* cand = (const uint2*)(D.h_fbuf + kFilterHeader);
             std::vector<uint2> more;
             if (nc > D.h_cand_cap) {
                 more.resize(nc);
-                check(hipMemcpy(more.data(), D.d_fbuf + 4, 8 * (size_t)nc, hipMemcpyDeviceToHost), "D2H candidates");
+                check(hipMemcpy(more.data(), D.d_fbuf + kFilterHeader, 8 * (size_t)nc, hipMemcpyDeviceToHost),
+                      "D2H candidates");
                 cand = more.data();
             }
+            // candidates by insertion position; out.cand holds view * E + entry
+            std::vector<uint2> cs(cand, cand + nc);
+            std::sort(cs.begin(), cs.end(), [](const uint2& x, const uint2& y) { return x.x < y.x; });
             out.cand.resize(nc);
             for (uint32_t i = 0; i < nc; i++) {
-                out.cand[i] = cand[i].x;
-                hs[cand[i].x] = (int32_t)cand[i].y;
+                const uint32_t x = multi ? D.h_order[cs[i].x] : cs[i].x;
+                out.cand[i] = x;
+                D.h_scores[x] = (int32_t)cs[i].y;
             }
-            std::sort(out.cand.begin(), out.cand.end());
             out.dev_o8 += D.h_fbuf[1];
             out.dev_o16 += D.h_fbuf[2];
-            if (nov > 0 && nov <= kOvfCap) {
-                check(hipMemcpy(D.h_ovf, D.d_ovf, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
-                check(hipMemcpy(D.h_wide, D.d_wide, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
+            for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
+                const uint32_t nov = D.h_fbuf[3 + vv];
+                if (nov) take_wide(multi ? vv : v, nov);
             }
         } else {
-            nov = D.h_ovf[0];
+            take_wide(v, D.h_ovf[0]);
         }
-        if (nov > kOvfCap) fatal("overflow list exhausted (%u entries)", nov);
-        if (!out.sparse && nov > 4096) {
-            check(hipMemcpy(D.h_ovf, D.d_ovf, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
-            check(hipMemcpy(D.h_wide, D.d_wide, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
-        }
-        for (uint32_t i = 0; i < nov; i++) {
-            const uint32_t e = D.lane_out[D.h_ovf[1 + i]];
-            out.wide[(uint64_t)v * E + e] = D.h_wide[i];
-        }
-        wide_total += nov;
         float t;
-        check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
-        kms += t;
-        check(hipEventElapsedTime(&t, D.ev[1], D.ev[2]), "elapsed");
+        if (multi) {
+            for (size_t vv = 0; vv < V; vv++) {
+                check(hipEventElapsedTime(&t, D.vev[2 * vv], D.vev[2 * vv + 1]), "elapsed");
+                kms += t;
+            }
+        } else {
+            check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
+            kms += t;
+        }
+        check(hipEventElapsedTime(&t, ev_k1, D.ev[2]), "elapsed");
         wms += t;
         check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
         dms += t;
         if (trace_on()) fprintf(stderr, "trace: post-sync %.3f\n", now_ms() - t_post0);
-        // algorithmic bytes: residues once + per-entry score write + profile
-        kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
     }
     if (trace_on())
         fprintf(stderr, "trace: prep %.3f sync %.3f total %.3f\n", prep, sync_wait, now_ms() - t_prep0);

@@ -56,6 +56,14 @@ struct DeviceDB {
     int64_t* h_wide = nullptr;            // pinned
     uint32_t* d_qpt = nullptr;
     size_t qpt_cap = 0;
+    size_t scores_cap = 0;                // d_scores entries
+    size_t filter_cap = 0;                // entries the filter buffers cover
+    // multi-view searches: insertion order of (view, entry) scores for the
+    // device filter (search_64.c:44-56 chunk interleave), device and host
+    uint32_t* d_order = nullptr;
+    std::vector<uint32_t> h_order;
+    uint64_t order_key = ~0ull;
+    std::vector<hipEvent_t> vev;          // per-view kernel start/end events
     uint32_t* d_top = nullptr;            // pair_kernel first-strip boundary quads
     size_t top_cap = 0;
     uint8_t* d_query = nullptr;

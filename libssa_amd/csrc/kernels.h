@@ -63,17 +63,24 @@ struct WideArgs {
 // the heap.  They are compacted into cand[] for the host replay.
 constexpr int kFilterBlock = 4096;
 constexpr int kFilterMaxK = 64;
+constexpr int kFilterMaxViews = 12;   // query views one filter pass covers
+constexpr int kFilterHeader = 16;     // dwords before the candidates in the counters buffer
 struct FilterArgs {
-    const int32_t* scores;     // [n] per-entry scores, INT32_MIN = overflowed (exact value elsewhere)
+    const int32_t* scores;     // per-entry scores, INT32_MIN = overflowed (exact value elsewhere)
+    const uint32_t* order;     // [n] score index of insertion position p (null: identity) -- the
+                               // chunk-interleaved order of multi-view searches
     uint32_t n, k, nblocks;
     int32_t nw, bw;            // counters follow the reference's overflow rules
     int32_t* summary;          // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
     int32_t* thresh;           // [nblocks] bound from earlier blocks
     int32_t* thresh_local;     // [nblocks * 64] bound from earlier minis of the same block
     int32_t* before;           // [nblocks][kFilterMaxK] scan scratch
-    const uint32_t* ovf_count; // copied into counters[3] (one host copy fetches everything)
-    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows, [3] overflowed lanes
-    uint2* cand;               // [n] (entry index, score) of the candidates, unordered; follows counters
+    const uint32_t* ovf_count; // view v's count at ovf_count[v * ovf_stride], copied into counters[3 + v]
+    uint32_t ovf_stride, nviews;
+    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows,
+                               // [3 + v] overflowed lanes of view v (one host copy fetches everything)
+    uint2* cand;               // [n] (insertion position, score) of the candidates, unordered;
+                               // at counters + kFilterHeader
 };
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 

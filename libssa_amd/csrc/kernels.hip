@@ -921,7 +921,7 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
     for (int i = 0; i < kMinisPerBlock / 4; i++) {
         const int m = i * 4 + wave;                 // this wave's mini: 64 consecutive entries
         const uint32_t e = base + m * kMini + lane;
-        const int32_t x = e < a.n ? a.scores[e] : INT32_MIN;
+        const int32_t x = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
         if (x != INT32_MIN) {
             if (!a.nw) {
                 my8 += a.bw == 8 && x >= 255;
@@ -1010,9 +1010,9 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
 
 __global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    if (e == 0) a.counters[3] = *a.ovf_count;
+    if (e < a.nviews) a.counters[3 + e] = a.ovf_count[(size_t)e * a.ovf_stride];
     if (e >= a.n) return;
-    const int32_t x = a.scores[e];
+    const int32_t x = a.scores[a.order ? a.order[e] : e];
     const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
     if (x == INT32_MIN || x > t) {
         const uint32_t i = atomicAdd(&a.counters[0], 1u);

@@ -531,6 +531,73 @@ def test_device_topk_filter_matches_full_scan(pattern):
         S.free_sequence(qq)
 
 
+@pytest.mark.parametrize("mode", ["both_strands", "trans_query"])
+def test_multiview_device_filter_matches_full_scan(mode):
+    """Multi-view searches (NUCLEOTIDE both strands: 2 query views;
+    TRANS_QUERY both strands: 6 frames) run every view back to back and one
+    device filter over all (view, entry) scores in the chunk-interleaved
+    insertion order; it must equal the host scan of every score (no_filter),
+    ties, overflow counters and insertion logs included."""
+    rng = np.random.default_rng(3)
+    if mode == "both_strands":
+        q = syn.dna_query(120, 4)
+        n = 20000
+        # short reads, many exact repeats of query pieces: heavy ties on both strands
+        seqs = [q[int(s):int(s) + 25].copy() if i % 3 else rng.choice(syn.NT_ACGT, 40).astype(np.uint8)
+                for i, s in enumerate(rng.integers(0, 90, n))]
+        codes = np.concatenate(seqs)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum([len(c) for c in seqs], out=off[1:])
+        S.set_output_mode(S.OUTPUT_ERROR)
+        S.init_symbol_translation(S.NUCLEOTIDE, S.BOTH_STRANDS, 1, 1)
+        S.init_constant_scores(2, -3)
+        S.init_gap_penalties(-5, -2)
+        qstr = syn.query_string(q, nucleotide=True)
+        nucleotide = True
+    else:
+        q = syn.dna_query(150, 5)
+        n = 15000
+        seqs = [rng.choice(syn.AA_CODES, int(rng.integers(5, 120))).astype(np.uint8) for _ in range(n)]
+        codes = np.concatenate(seqs)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum([len(c) for c in seqs], out=off[1:])
+        S.set_output_mode(S.OUTPUT_ERROR)
+        S.init_symbol_translation(S.TRANS_QUERY, S.BOTH_STRANDS, 1, 1)
+        S.init_score_matrix(S.MATRIX_BUILDIN, "blosum62")
+        S.init_gap_penalties(-11, -1)
+        qstr = syn.query_string(q, nucleotide=True)
+        nucleotide = False
+    try:
+        for chunk in (1000, 37):
+            S.set_chunk_size(chunk)
+            with tempfile.TemporaryDirectory() as tmp:
+                path = os.path.join(tmp, "db.fas")
+                syn.write_fasta(path, codes, off, nucleotide=nucleotide)
+                S.init_db(path)
+                qq = S.init_sequence_fasta(S.READ_FROM_STRING, qstr)
+                for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+                    for k in (1, 10, 64):
+                        for width in (8, 16):
+                            S.set_option("no_filter", 1)
+                            full = [(h["score"], h["id"]) for h in fn(qq, k, width)]
+                            st_full = S.stats()
+                            S.set_option("no_filter", 0)
+                            got = [(h["score"], h["id"]) for h in fn(qq, k, width)]
+                            st = S.stats()
+                            assert got == full, (mode, chunk, algo, k, width, got[:4], full[:4])
+                            assert (st["overflow_8"], st["overflow_16"]) == \
+                                (st_full["overflow_8"], st_full["overflow_16"])
+                    S.set_option("no_filter", 1)
+                    log_full = S.search(qq, algo, 9, 16, S.LOG)
+                    S.set_option("no_filter", 0)
+                    assert S.search(qq, algo, 9, 16, S.LOG) == log_full
+                S.free_sequence(qq)
+    finally:
+        S.set_option("no_filter", 0)
+        S.set_chunk_size(1000)
+        S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+
+
 def test_packed_db_save_load_roundtrip(tmp_path):
     """ssa_amd_save_db / ssa_amd_load_db: a reloaded packed DB gives the same
     results as packing from the plugin (protein, and NUCLEOTIDE with both
