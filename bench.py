@@ -194,8 +194,8 @@ def main():
 
     def step():
         if world == 1:
-            fn = S.sw_align if algo == S.SW else S.nw_align
-            return [(h["score"], h["id"]) for h in fn(qq, args.k, args.width)]
+            # the public sw_align / nw_align + free_alignment (libssa.h)
+            return S.align_scores(qq, args.k, args.width, algo)
         from libssa_amd.dist import global_topk
         log = S.search(qq, algo, args.k, args.width, S.LOG)
         return global_topk(log, args.k, dist, rank, world, dev)

@@ -175,6 +175,24 @@ def sw_align(q, hitcount, bit_width=BIT_WIDTH_16, align_type=COMPUTE_SCORE):
     return res
 
 
+def align_scores(q, hitcount, bit_width=BIT_WIDTH_16, algo=SW):
+    """sw_align / nw_align (COMPUTE_SCORE) + free_alignment, exactly the
+    public calls the reference's benchmark times (benchmark_util.c:27-48),
+    returning only [(score, db_id)] -- reading two fields per hit keeps the
+    Python side to a few microseconds (bench.py's timed step)."""
+    L = load()
+    al = (L.sw_align if algo == SW else L.nw_align)(q, hitcount, bit_width, COMPUTE_SCORE)
+    out = []
+    if al:
+        a = al.contents
+        arr = a.alignments
+        for i in range(a.len):
+            x = arr[i].contents
+            out.append((x.score, x.db_seq.ID))
+    L.free_alignment(al)
+    return out
+
+
 def nw_align(q, hitcount, bit_width=BIT_WIDTH_16, align_type=COMPUTE_SCORE):
     L = load()
     al = L.nw_align(q, hitcount, bit_width, align_type)
@@ -201,8 +219,11 @@ def save_db(path): return load().ssa_amd_save_db(_b(path))
 def load_db(path): return load().ssa_amd_load_db(_b(path))
 
 
+_stats_buf = ssa_amd_stats_t()
+
+
 def stats():
-    s = ssa_amd_stats_t()
+    s = _stats_buf
     load().ssa_amd_get_stats(ctypes.byref(s))
     d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
     d["kernel"] = d["kernel"].decode()
