@@ -451,6 +451,68 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
     const double t0 = now_ms();
     double kms = 0;
     uint64_t cells = 0;
+    // single-device, single-view queries with a small k: pipelined sub-batches
+    // (device_search's independent mode) -- the host prepares query i+1 while
+    // query i runs, one synchronisation per sub-batch
+    const int al = algo == SSA_AMD_NW ? kAlgoNW : kAlgoSW;
+    bool piped = nq > 1 && batch_pipelinable(nq, hitcount);
+    std::vector<std::vector<QueryView>> qviews(piped ? nq : 0);
+    for (size_t i = 0; piped && i < nq; i++) {
+        test_configuration(queries[i]);
+        qviews[i] = query_views(queries[i]);
+        piped = qviews[i].size() == 1 && qviews[i][0].len > 0;
+    }
+    if (piped) {
+        check_width(bit_width);
+        ensure_device_db();
+        piped = device_plan().size() == 1;
+    }
+    if (piped) {
+        DeviceDB& D = device_db(0);
+        for (size_t b0 = 0; b0 < nq; b0 += kMaxBatchPipe) {
+            const size_t b1 = std::min(nq, b0 + kMaxBatchPipe);
+            std::vector<QueryView> vs;
+            for (size_t i = b0; i < b1; i++) vs.push_back(qviews[i][0]);
+            if (vs.size() == 1) {
+                // a lone last query: the ordinary path
+                SearchResult R;
+                run_search(queries[b0], al, hitcount, bit_width, false, R);
+                kms += stats().kernel_ms;
+                cells += stats().cells;
+                const size_t n = std::min(hitcount, R.hits.size());
+                for (size_t j = 0; j < n; j++) {
+                    const Hit& h = R.hits[j];
+                    out[b0 * hitcount + j] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
+                }
+                if (counts) counts[b0] = n;
+                total += n;
+                continue;
+            }
+            SearchScores agg;
+            std::vector<SearchScores> sc;
+            device_search(D, vs, al, hitcount, bit_width, agg, &sc);
+            kms += agg.kernel_ms;
+            for (size_t i = b0; i < b1; i++) {
+                const SearchScores& x = sc[i - b0];
+                cells += x.cells;
+                TopK heap(hitcount);
+                replay(x, D.meta, qviews[i], heap, nullptr);
+                const std::vector<Hit> hits = heap.sorted();
+                const size_t n = std::min(hitcount, hits.size());
+                for (size_t j = 0; j < n; j++) {
+                    const Hit& h = hits[j];
+                    out[i * hitcount + j] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
+                }
+                if (counts) counts[i] = n;
+                total += n;
+            }
+        }
+        ssa_amd_stats_t& S = stats();
+        S.kernel_ms = kms;
+        S.cells = cells;
+        S.search_ms = now_ms() - t0;
+        return total;
+    }
     for (size_t i = 0; i < nq; i++) {
         test_configuration(queries[i]);
         SearchResult R;

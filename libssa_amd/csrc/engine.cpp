@@ -329,6 +329,8 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         const size_t nb = (E + kFilterBlock - 1) / kFilterBlock;
         dalloc((void**)&D.d_fbuf, kFilterHeader * 4 + std::max<size_t>(E, 1) * 8, "filter candidates");
         D.filter_cap = std::max<size_t>(E, 1);
+        D.fbuf_bytes = kFilterHeader * 4 + std::max<size_t>(E, 1) * 8;
+        D.h_fbuf_regions = 1;
         dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
         dalloc((void**)&D.d_before, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter scan");
         dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
@@ -623,7 +625,12 @@ static uint32_t sw_rel_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM)
     return (uint32_t)a;
 }
 
-void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out) {
+bool batch_pipelinable(size_t nqueries, size_t k) {
+    return nqueries > 1 && k > 0 && k <= (size_t)kFilterMaxK && !cfg().no_filter;
+}
+
+void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out,
+                   std::vector<SearchScores>* indep) {
     check(hipSetDevice(D.device), "hipSetDevice");
     const Config& C = cfg();
     const size_t E = D.meta.size();
@@ -658,18 +665,47 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     // slice, then one filter pass over all (view, entry) scores in the
     // reference's chunk-interleaved insertion order -- no per-view sync,
     // copy or host scan of every score
-    const bool multi = out.sparse && V > 1;
-    const size_t ovf_capv = multi ? kOvfCap / V - 1 : kOvfCap;
-    if (multi) {
+    // independent queries (a batch): the same back-to-back enqueue, but
+    // every query gets its own filter pass, candidate region and result
+    const bool ind = indep != nullptr;
+    if (ind && !(out.sparse && V > 1 && V <= kMaxBatchPipe)) fatal("device_search: batch not pipelinable");
+    const bool multi = out.sparse && V > 1 && !ind;
+    const bool piped = multi || ind;
+    const size_t ovf_capv = piped ? kOvfCap / V - 1 : kOvfCap;
+    // pipelined: per-query candidate regions (device and pinned host)
+    const size_t dreg = ind ? ((size_t)kFilterHeader * 4 + E * 8 + 255) & ~(size_t)255 : 0;
+    const size_t hreg = (size_t)kFilterHeader * 4 + D.h_cand_cap * 8;
+    if (piped) {
         if (D.scores_cap < V * E) {
             dfree(D.d_scores);
             check(hipMalloc((void**)&D.d_scores, V * E * 4), "scores");
             D.scores_cap = V * E;
         }
+        while (D.vev.size() < 2 * V) {
+            hipEvent_t e;
+            check(hipEventCreate(&e), "hipEventCreate");
+            D.vev.push_back(e);
+        }
+    }
+    if (ind) {
+        if (D.fbuf_bytes < V * dreg) {
+            dfree(D.d_fbuf);
+            check(hipMalloc((void**)&D.d_fbuf, V * dreg), "filter candidates");
+            D.fbuf_bytes = V * dreg;
+        }
+        if (D.h_fbuf_regions < V) {
+            if (D.h_fbuf) (void)hipHostFree(D.h_fbuf);
+            check(hipHostMalloc((void**)&D.h_fbuf, V * hreg, hipHostMallocDefault), "pinned candidates");
+            D.h_fbuf_regions = V;
+        }
+        indep->assign(V, SearchScores{});
+    }
+    if (multi) {
         if (D.filter_cap < V * E) {
             const size_t nb = (V * E + kFilterBlock - 1) / kFilterBlock;
             dfree(D.d_fbuf); dfree(D.d_summary); dfree(D.d_before); dfree(D.d_thresh_local); dfree(D.d_thresh);
             check(hipMalloc((void**)&D.d_fbuf, kFilterHeader * 4 + V * E * 8), "filter candidates");
+            D.fbuf_bytes = kFilterHeader * 4 + V * E * 8;
             check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 4), "filter summaries");
             check(hipMalloc((void**)&D.d_before, nb * kFilterMaxK * 4), "filter scan");
             check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
@@ -695,11 +731,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMalloc((void**)&D.d_order, V * E * 4), "insertion order");
             check(hipMemcpy(D.d_order, D.h_order.data(), V * E * 4, hipMemcpyHostToDevice), "H2D order");
             D.order_key = key;
-        }
-        while (D.vev.size() < 2 * V) {
-            hipEvent_t e;
-            check(hipEventCreate(&e), "hipEventCreate");
-            D.vev.push_back(e);
         }
     }
     float kms = 0, wms = 0, dms = 0;
@@ -867,7 +898,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         // the staging buffer is reused: in a multi-view search the previous
         // view's copies may still be queued behind its predecessor's kernel
-        if (multi && v > 0) check(hipEventSynchronize(D.ev[5]), "staging");
+        if (piped && v > 0) check(hipEventSynchronize(D.ev[5]), "staging");
         uint8_t* up_q = D.h_up;
         uint8_t* up_t = up_q + qpt.size() * 4;
         uint8_t* up_m = up_t + top.size() * 4;
@@ -883,7 +914,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMemcpyAsync(D.d_top, up_t, top.size() * 4, hipMemcpyHostToDevice, st), "H2D top");
         check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
         check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
-        if (multi) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
+        if (piped) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
         if (use_pair) {
             TableArgs ta{};
             ta.query = D.d_query;
@@ -901,8 +932,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         // overflow list of this view: the whole list, or in a multi-view
         // search its own slice (all views stay on the device until the end)
-        uint32_t* ovf = D.d_ovf + (multi ? v * (ovf_capv + 1) : 0);
-        int64_t* wide = D.d_wide + (multi ? v * ovf_capv : 0);
+        uint32_t* ovf = D.d_ovf + (piped ? v * (ovf_capv + 1) : 0);
+        int64_t* wide = D.d_wide + (piped ? v * ovf_capv : 0);
         check(hipMemsetAsync(ovf, 0, 4, st), "memset");
 
         StripArgs a{};
@@ -912,7 +943,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         a.lane_len = D.d_lane_len;
         a.lane_out = D.d_lane_out;
         a.qpt = D.d_qpt;
-        a.scores = D.d_scores + (multi ? v * E : 0);
+        a.scores = D.d_scores + (piped ? v * E : 0);
         a.ovf_list = ovf + 1;
         a.ovf_count = ovf;
         a.ngroups = D.ngroups;
@@ -946,7 +977,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
         if (v == 0) prep = now_ms() - t_prep0;
-        hipEvent_t ev_k0 = multi ? D.vev[2 * v] : D.ev[0], ev_k1 = multi ? D.vev[2 * v + 1] : D.ev[1];
+        hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         check(hipEventRecord(ev_k0, st), "event");
         if (use_pair) {
             StripArgs b = a;
@@ -961,9 +992,36 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         check(hipEventRecord(ev_k1, st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
-        if (multi && v + 1 < V) continue;
+        if (ind) {
+            // this query's own filter pass into its own candidate region
+            uint32_t* reg = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
+            FilterArgs f{};
+            f.scores = D.d_scores + v * E;
+            f.order = nullptr;
+            f.n = (uint32_t)E;
+            f.k = (uint32_t)k;
+            f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
+            f.nw = nw ? 1 : 0;
+            f.bw = bw;
+            f.summary = D.d_summary;
+            f.thresh = D.d_thresh;
+            f.thresh_local = D.d_thresh_local;
+            f.before = D.d_before;
+            f.ovf_count = ovf;
+            f.ovf_stride = 0;
+            f.nviews = 1;
+            f.counters = reg;
+            f.cand = (uint2*)(reg + kFilterHeader);
+            check(hipMemsetAsync(reg, 0, kFilterHeader * 4, st), "memset");
+            check(launch_filter(f, st), "filter launch");
+            check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
+                                 hipMemcpyDeviceToHost, st), "D2H candidates");
+        }
+        if (piped && v + 1 < V) continue;
         check(hipEventRecord(D.ev[2], st), "event");
-        if (out.sparse) {
+        if (ind) {
+            // (filters already enqueued per query)
+        } else if (out.sparse) {
             FilterArgs f{};
             f.scores = D.d_scores;
             f.order = multi ? D.d_order : nullptr;
@@ -1004,21 +1062,50 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             upload += u;
         }
         // exact int64 scores of overflowed lanes: view vv's list and scores
-        auto take_wide = [&](size_t vv, uint32_t nov) {
+        auto take_wide = [&](size_t vv, uint32_t nov, SearchScores& dst, size_t key_view) {
             if (nov > ovf_capv) fatal("overflow list exhausted (%u entries)", nov);
-            const uint32_t* ov = D.d_ovf + (multi ? vv * (ovf_capv + 1) : 0);
-            const int64_t* wd = D.d_wide + (multi ? vv * ovf_capv : 0);
+            const uint32_t* ov = D.d_ovf + (piped ? vv * (ovf_capv + 1) : 0);
+            const int64_t* wd = D.d_wide + (piped ? vv * ovf_capv : 0);
             if (out.sparse || nov > 4096) {
                 check(hipMemcpy(D.h_ovf, ov, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
                 check(hipMemcpy(D.h_wide, wd, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
             }
             for (uint32_t i = 0; i < nov; i++) {
                 const uint32_t e = D.lane_out[D.h_ovf[1 + i]];
-                out.wide[(uint64_t)vv * E + e] = D.h_wide[i];
+                dst.wide[(uint64_t)key_view * E + e] = D.h_wide[i];
             }
             wide_total += nov;
         };
-        if (out.sparse) {
+        if (ind) {
+            for (size_t vv = 0; vv < V; vv++) {
+                SearchScores& o = (*indep)[vv];
+                const uint32_t* hf = (const uint32_t*)((const uint8_t*)D.h_fbuf + vv * hreg);
+                const uint32_t nc = hf[0];
+                const uint2* cand = (const uint2*)(hf + kFilterHeader);
+                std::vector<uint2> more;
+                if (nc > D.h_cand_cap) {
+                    more.resize(nc);
+                    check(hipMemcpy(more.data(), (const uint8_t*)D.d_fbuf + vv * dreg + kFilterHeader * 4, 8 * (size_t)nc,
+                                    hipMemcpyDeviceToHost), "D2H candidates");
+                    cand = more.data();
+                }
+                o.s32 = D.h_scores + vv * E;
+                o.entries = E;
+                o.views = 1;
+                o.sparse = true;
+                o.cells = (uint64_t)views[vv].len * D.meta.residues;
+                o.cand.resize(nc);
+                for (uint32_t i = 0; i < nc; i++) {
+                    o.cand[i] = cand[i].x;
+                    D.h_scores[vv * E + cand[i].x] = (int32_t)cand[i].y;
+                }
+                std::sort(o.cand.begin(), o.cand.end());
+                o.dev_o8 = hf[1];
+                o.dev_o16 = hf[2];
+                if (hf[3]) take_wide(vv, hf[3], o, 0);
+                o.kernel = kname;
+            }
+        } else if (out.sparse) {
             const uint32_t nc = D.h_fbuf[0];
             const uint2* cand = (const uint2*)(D.h_fbuf + kFilterHeader);
             std::vector<uint2> more;
@@ -1041,16 +1128,17 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             out.dev_o16 += D.h_fbuf[2];
             for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
                 const uint32_t nov = D.h_fbuf[3 + vv];
-                if (nov) take_wide(multi ? vv : v, nov);
+                if (nov) take_wide(multi ? vv : v, nov, out, multi ? vv : v);
             }
         } else {
-            take_wide(v, D.h_ovf[0]);
+            take_wide(v, D.h_ovf[0], out, v);
         }
         float t;
-        if (multi) {
+        if (piped) {
             for (size_t vv = 0; vv < V; vv++) {
                 check(hipEventElapsedTime(&t, D.vev[2 * vv], D.vev[2 * vv + 1]), "elapsed");
                 kms += t;
+                if (ind) (*indep)[vv].kernel_ms = t;
             }
         } else {
             check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");

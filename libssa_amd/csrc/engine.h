@@ -64,6 +64,8 @@ struct DeviceDB {
     std::vector<uint32_t> h_order;
     uint64_t order_key = ~0ull;
     std::vector<hipEvent_t> vev;          // per-view kernel start/end events
+    size_t fbuf_bytes = 0;                // d_fbuf capacity
+    size_t h_fbuf_regions = 1;            // pinned h_fbuf regions (one per pipelined query)
     uint32_t* d_top = nullptr;            // pair_kernel first-strip boundary quads
     size_t top_cap = 0;
     uint8_t* d_query = nullptr;
@@ -124,7 +126,15 @@ struct SearchScores {
     }
 };
 // k / bit_width decide whether the device top-k filter applies
-void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out);
+// indep != null: every view is an independent single-view query
+// (ssa_amd_search_batch): the queries are enqueued back to back, each with its
+// own device filter pass, and (*indep)[v] receives query v's scores; `out`
+// then only carries the batch's aggregate timing.  Callers check
+// batch_pipelinable() first.
+void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out,
+                   std::vector<SearchScores>* indep = nullptr);
+bool batch_pipelinable(size_t nqueries, size_t k);
+constexpr size_t kMaxBatchPipe = 8;     // queries per pipelined sub-batch
 
 ssa_amd_stats_t& stats();
 void check(hipError_t e, const char* what);

@@ -732,6 +732,37 @@ def test_search_batch_matches_single_queries():
             S.free_sequence(q)
 
 
+def test_search_batch_pipelined_sub_batches():
+    """Batches beyond one pipelined sub-batch (8 queries), every k up to the
+    device filter's 64, a lone last query, and overflowing queries (int64
+    re-score inside a pipelined batch) -- each equal to its single search."""
+    codes, off = syn.protein_db(4000, 22, lo=1, hi=700)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        lens = (3, 17, 30, 48, 49, 96, 100, 150, 233, 400, 401, 7, 64, 300, 20, 55, 90)
+        qs = [S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(syn.protein_query(n, 100 + n)))
+              for n in lens]
+        for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+            for k in (1, 7, 64):
+                for sub in (qs, qs[:9], qs[:2]):
+                    exp = [[(h["score"], h["id"]) for h in fn(q, k, 16)] for q in sub]
+                    assert S.search_batch(sub, algo, k) == exp, (algo, k, len(sub))
+        for q in qs:
+            S.free_sequence(q)
+    # scores beyond the 16-bit range: re-scored by the int64 kernel per query
+    configure(False, ("const", 127, -1), -1, -1)
+    S.init_db(os.path.join(DATA, "NP_009305.1.fas"))
+    qa = S.init_sequence_fasta(S.READ_FROM_FILE, os.path.join(DATA, "NP_009305.1.fas"))
+    qb = S.init_sequence_fasta(S.READ_FROM_STRING, "MKTAYIAKQRQISFVKSHFSRQ")
+    for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+        exp = [[(h["score"], h["id"]) for h in fn(q, 1, 16)] for q in (qa, qb, qa)]
+        assert exp[0] == [(67818, 0)]
+        assert S.search_batch([qa, qb, qa], algo, 1) == exp
+    S.free_sequence(qa)
+    S.free_sequence(qb)
+
+
 CLI = os.path.join(os.path.dirname(po.__file__), "_ref", "libssa_example_amd")
 
 
