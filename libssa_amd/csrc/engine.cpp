@@ -43,8 +43,10 @@ static void dfree(void* p) {
 void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
-    dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_query); dfree(d_matrix);
-    dfree(d_work); dfree(d_top); dfree(d_order);
+    dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
+    dfree(d_work); dfree(d_order);
+    d_upblk = nullptr;
+    upblk_cap = 0;
     d_order = nullptr;
     h_order.clear();
     order_key = ~0ull;
@@ -52,7 +54,6 @@ void DeviceDB::release() {
     for (auto& e : vev) (void)hipEventDestroy(e);
     vev.clear();
     d_top = nullptr;
-    top_cap = 0;
     dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
     if (h_fbuf) (void)hipHostFree(h_fbuf);
     if (h_up) (void)hipHostFree(h_up);
@@ -67,7 +68,7 @@ void DeviceDB::release() {
     d_groups = nullptr; d_res = nullptr; d_rowbuf = nullptr; d_lane_len = nullptr; d_lane_out = nullptr;
     d_scores = nullptr; d_ovf = nullptr; d_wide = nullptr; d_qpt = nullptr; d_query = nullptr;
     d_matrix = nullptr; d_work = nullptr; h_scores = nullptr; h_ovf = nullptr; h_wide = nullptr;
-    h_scores_cap = qpt_cap = query_cap = work_cap = 0;
+    h_scores_cap = qpt_cap = work_cap = 0;
     generation = ~0ull;
     meta = EntryMeta();
     lane_out.clear();
@@ -342,7 +343,9 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     D.scores_cap = std::max<size_t>(E, 1);
     dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
     dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
-    dalloc((void**)&D.d_matrix, 1024 * 8, "matrix");
+    D.upblk_cap = 8192 + 16384 + 4096;
+    dalloc((void**)&D.d_upblk, D.upblk_cap, "per-search uploads");
+    D.d_matrix = (int64_t*)D.d_upblk;
     check(hipHostMalloc((void**)&D.h_ovf, (kOvfCap + 1) * 4, hipHostMallocDefault), "pinned");
     check(hipHostMalloc((void**)&D.h_wide, kOvfCap * 8, hipHostMallocDefault), "pinned");
     check(hipMemcpy(D.d_groups, H.groups.data(), H.groups.size() * sizeof(GroupDesc), hipMemcpyHostToDevice), "H2D");
@@ -851,11 +854,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMalloc((void**)&D.d_qpt, qpt_words * 4), "qpt");
             D.qpt_cap = qpt_words;
         }
-        if (D.query_cap < m) {
-            dfree(D.d_query);
-            check(hipMalloc((void**)&D.d_query, m), "query");
-            D.query_cap = m;
-        }
+
         const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
         if (D.work_cap < (size_t)wide_threads * 2 * m) {
             dfree(D.d_work);
@@ -883,14 +882,20 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
             }
         }
-        if (D.top_cap < top.size()) {
-            dfree(D.d_top);
-            check(hipMalloc((void**)&D.d_top, top.size() * 4), "top boundary");
-            D.top_cap = top.size();
+        // device upload block: [matrix 8 KB][top boundary][query codes]
+        const size_t top_bytes = (top.size() * 4 + 15) & ~(size_t)15;
+        const size_t blk_bytes = 8192 + top_bytes + m;
+        if (D.upblk_cap < blk_bytes) {
+            dfree(D.d_upblk);
+            D.upblk_cap = blk_bytes + 4096;
+            check(hipMalloc((void**)&D.d_upblk, D.upblk_cap), "per-search uploads");
         }
+        D.d_matrix = (int64_t*)D.d_upblk;
+        D.d_top = (uint32_t*)(D.d_upblk + 8192);
+        D.d_query = D.d_upblk + 8192 + top_bytes;
         // one pinned staging buffer for the per-search uploads (pageable
         // sources would make each copy a synchronous staged transfer)
-        const size_t up_bytes = qpt.size() * 4 + top.size() * 4 + 1024 * 8 + ((m + 15) & ~(size_t)15);
+        const size_t up_bytes = blk_bytes + 16 + qpt.size() * 4;
         if (D.h_up_cap < up_bytes) {
             if (D.h_up) (void)hipHostFree(D.h_up);
             check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
@@ -899,22 +904,24 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // the staging buffer is reused: in a multi-view search the previous
         // view's copies may still be queued behind its predecessor's kernel
         if (piped && v > 0) check(hipEventSynchronize(D.ev[5]), "staging");
-        uint8_t* up_q = D.h_up;
-        uint8_t* up_t = up_q + qpt.size() * 4;
-        uint8_t* up_m = up_t + top.size() * 4;
-        uint8_t* up_s = up_m + 1024 * 8;
-        if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
-        if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
+        // staging mirrors the device block, then the strip kernels' table
+        uint8_t* up_m = D.h_up;
+        uint8_t* up_t = up_m + 8192;
+        uint8_t* up_s = up_t + top_bytes;
+        uint8_t* up_q = D.h_up + ((blk_bytes + 15) & ~(size_t)15);
         memcpy(up_m, Mc, 1024 * 8);
+        if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_s, qv.seq, m);
+        if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
         check(hipEventRecord(D.ev[4], st), "event");
         if (!qpt.empty())
             check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
-        if (!top.empty())
-            check(hipMemcpyAsync(D.d_top, up_t, top.size() * 4, hipMemcpyHostToDevice, st), "H2D top");
-        check(hipMemcpyAsync(D.d_query, up_s, m, hipMemcpyHostToDevice, st), "H2D query");
-        check(hipMemcpyAsync(D.d_matrix, up_m, 1024 * 8, hipMemcpyHostToDevice, st), "H2D matrix");
+        check(hipMemcpyAsync(D.d_upblk, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
         if (piped) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
+        // overflow list of this view: the whole list, or in a multi-view
+        // search its own slice (all views stay on the device until the end)
+        uint32_t* ovf = D.d_ovf + (piped ? v * (ovf_capv + 1) : 0);
+        int64_t* wide = D.d_wide + (piped ? v * ovf_capv : 0);
         if (use_pair) {
             TableArgs ta{};
             ta.query = D.d_query;
@@ -928,13 +935,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.tail_row0 = main_strips * 2 * (uint32_t)pnp;
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
+            ta.zero = ovf;
             check(launch_pair_tables(ta, st), "pair tables kernel");
+        } else {
+            check(hipMemsetAsync(ovf, 0, 4, st), "memset");
         }
-        // overflow list of this view: the whole list, or in a multi-view
-        // search its own slice (all views stay on the device until the end)
-        uint32_t* ovf = D.d_ovf + (piped ? v * (ovf_capv + 1) : 0);
-        int64_t* wide = D.d_wide + (piped ? v * ovf_capv : 0);
-        check(hipMemsetAsync(ovf, 0, 4, st), "memset");
 
         StripArgs a{};
         a.res = D.d_res;
@@ -972,6 +977,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         w.gap_extend = R;
         w.nw = nw ? 1 : 0;
         w.ovf_cap = (uint32_t)ovf_capv;
+        // the counters of the filter pass that follows this wide kernel
+        if (ind) w.zero = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
+        else if (out.sparse && v + 1 == V) w.zero = D.d_fbuf;
+        w.nzero = w.zero ? kFilterHeader : 0;
 
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
@@ -1012,7 +1021,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             f.nviews = 1;
             f.counters = reg;
             f.cand = (uint2*)(reg + kFilterHeader);
-            check(hipMemsetAsync(reg, 0, kFilterHeader * 4, st), "memset");
             check(launch_filter(f, st), "filter launch");
             check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
                                  hipMemcpyDeviceToHost, st), "D2H candidates");
@@ -1039,7 +1047,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             f.nviews = (uint32_t)(multi ? V : 1);
             f.counters = D.d_fbuf;
             f.cand = (uint2*)(D.d_fbuf + kFilterHeader);
-            check(hipMemsetAsync(D.d_fbuf, 0, kFilterHeader * 4, st), "memset");
             check(launch_filter(f, st), "filter launch");
             // one copy: counters (incl. the overflow counts) + the first candidates
             const size_t first = std::min<size_t>(D.h_cand_cap, f.n);

@@ -66,10 +66,13 @@ struct DeviceDB {
     std::vector<hipEvent_t> vev;          // per-view kernel start/end events
     size_t fbuf_bytes = 0;                // d_fbuf capacity
     size_t h_fbuf_regions = 1;            // pinned h_fbuf regions (one per pipelined query)
-    uint32_t* d_top = nullptr;            // pair_kernel first-strip boundary quads
-    size_t top_cap = 0;
+    // per-search uploads in one device block (one H2D copy): the compact-code
+    // matrix, the pair kernel's first-strip boundary quads, the query codes;
+    // d_matrix / d_top / d_query point into it (not separately owned)
+    uint8_t* d_upblk = nullptr;
+    size_t upblk_cap = 0;
+    uint32_t* d_top = nullptr;
     uint8_t* d_query = nullptr;
-    size_t query_cap = 0;
     int64_t* d_matrix = nullptr;
     int64_t* d_work = nullptr;
     size_t work_cap = 0;

@@ -54,6 +54,8 @@ struct WideArgs {
     int32_t gap_open, gap_extend;
     int32_t nw;
     uint32_t ovf_cap;
+    uint32_t* zero;            // nzero dwords cleared by block 0 (the next filter pass's counters)
+    uint32_t nzero;
 };
 
 // Device-side top-k candidate filter (single query view, k <= kFilterMaxK).
@@ -105,6 +107,7 @@ struct TableArgs {
     uint32_t npt, tail_row0;   // tail strip half-height (0: none) and first row
     int32_t rel;               // added to every real profile value (-2R)
     uint32_t pad;              // 16-bit padding value
+    uint32_t* zero;            // cleared by thread 0 (the search's overflow count), may be null
 };
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
 

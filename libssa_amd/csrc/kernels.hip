@@ -810,6 +810,7 @@ pair_kernel(const StripArgs a) {
 // Exact int64 re-score of overflowed lanes: the reference's 64-bit
 // recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
+    if (blockIdx.x == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x] = 0;
     const uint32_t n = min(*a.ovf_count, a.ovf_cap);
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1038,6 +1039,7 @@ __device__ __forceinline__ uint32_t table_val(const TableArgs& a, uint32_t c, ui
 }
 
 __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
+    if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;
     const uint32_t prow = a.alpha + 1;
     const uint32_t per_main = prow * prow * a.np;
     const uint32_t nmain = a.nmain * per_main;
@@ -1062,7 +1064,7 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const uint32_t prow = a.alpha + 1;
     const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);
-    if (total == 0) return hipSuccess;
+    if (total == 0) return a.zero ? hipMemsetAsync(a.zero, 0, 4, st) : hipSuccess;
     const uint32_t blocks = (uint32_t)std::min<size_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(pair_tables_kernel, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
