@@ -674,7 +674,11 @@ pair_kernel(const StripArgs a) {
                     uint32_t xs[2];
 #pragma unroll
                     for (int r = 0; r < NPS; r++) {
-                        const uint32_t h = fmax3(padd16(hd, P[r]), E[r], F);
+                        // the diagonal step: P holds combined signed constants
+                        // (pair_tables_kernel), so one full-rate v_add_u32
+                        // replaces the half-rate v_pk_add_u16 (-5 % per row,
+                        // profiles/r01/ubench_mix_rates.txt)
+                        const uint32_t h = fmax3(hd + P[r], E[r], F);
                         if ((r & 3) == 3) {
                             const uint4 v = *(const uint4*)(nrow + r - 3);
                             P[r - 3] = v.x;
@@ -1031,11 +1035,11 @@ hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
 
 // Per-search pair tables for pair_kernel (kernels.h TableArgs): one thread
 // per dword, replacing a host build + a ~400 KB upload per search.
-__device__ __forceinline__ uint32_t table_val(const TableArgs& a, uint32_t c, uint32_t i) {
-    if (c >= a.alpha || i >= a.m) return a.pad;
+__device__ __forceinline__ int32_t table_val(const TableArgs& a, uint32_t c, uint32_t i) {
+    if (c >= a.alpha || i >= a.m) return (int32_t)(int16_t)a.pad;
     int64_t v = a.matrix[(c << 5) + a.query[i]] + a.rel;
     v = v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
-    return (uint32_t)(uint16_t)(int16_t)v;
+    return (int32_t)v;
 }
 
 __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
@@ -1057,7 +1061,10 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
         }
         const uint32_t pair = rem / ph, r = rem % ph;
         const uint32_t c1 = pair / prow, c0 = pair % prow;
-        a.out[t] = table_val(a, c1, i0 + r) | (table_val(a, c0, i0 + ph + r) << 16);
+        // "combined" signed constant lo + 65536 hi: one v_add_u32 adds it to a
+        // packed pair of patterns exactly as two 16-bit adds would, since the
+        // low half's sum never leaves [0, 0xFFFF] (pair_kernel's bounds)
+        a.out[t] = (uint32_t)(table_val(a, c0, i0 + ph + r) * 65536 + table_val(a, c1, i0 + r));
     }
 }
 

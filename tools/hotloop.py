@@ -28,9 +28,9 @@ for line in s[i:j].split('\n'):
 blocks.append(cur)
 tot = Counter()
 for b in blocks:
-    if b['v_pk_add_u16'] >= rows // 2 and b['v_pk_maximum3_f16'] >= rows:
+    if b['v_pk_maximum3_f16'] >= 2 * rows:
         tot.update(b)
-cols = tot['v_pk_add_u16'] / rows
+cols = tot['ds_read_b128'] / (rows / 4)     # each column loads its next pair row
 valu = sum(v for k, v in tot.items() if k.startswith('v_'))
 print(f"{name}: {cols:.0f} columns, VALU/column {valu / cols:.1f}, VALU/cell {valu / cols / (2 * rows):.3f}")
 print("  per column:", {k: round(v / cols, 2) for k, v in sorted(tot.items(), key=lambda x: -x[1])})
