@@ -12,13 +12,15 @@ N>1 each rank searches its own 1 M-sequence shard of an N M-sequence DB
 log, the logs are gathered to rank 0 over RCCL and replayed there
 (ssa_amd_replay), giving the bit-exact global result.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--seqs S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|ref] [--seqs S]
 
 Other BASELINE.json configurations (parity/extra measurements; the default
 line is C2): --config c3 = NW BLOSUM50 -10/-2, 1000-residue query, 1 M
 sequences per GPU; c4 = SW BLOSUM62 -11/-1 (API width 8) over 10 M sequences
 split across the ranks (strong scaling); c5 = SW DNA +5/-4, gaps -4/-2,
-10 k-nt query vs 50 M reads of 150 nt split across the ranks (strong).
+10 k-nt query vs 50 M reads of 150 nt split across the ranks (strong); ref =
+the reference's published benchmark shape (P18080, 513 aa, BLOSUM50 -3/-1,
+548,208 synthetic sequences).
 --seqs overrides the per-GPU sequence count of any config.
 """
 import argparse
@@ -87,7 +89,22 @@ CONFIGS = {
                seqs=None, total_seqs=10_000_000, width=8),
     "c5": dict(algo="sw", matrix="const5_-4", gap_open=-4, gap_extend=-2, qlen=10_000, db="dna",
                seqs=None, total_seqs=50_000_000, width=16),
+    # the shape of the reference's own published benchmark (BASELINE.md §1:
+    # query P18080, 513 aa, BLOSUM50, gaps -3/-1, UniProtKB/Swiss-Prot
+    # 2015_03 = 548,208 sequences; benchmark/src/benchmark_threads.c:36-46),
+    # on a synthetic DB of that sequence count (no network for Swiss-Prot)
+    "ref": dict(algo="sw", matrix="blosum50", gap_open=-3, gap_extend=-1, qlen=513, db="protein",
+                seqs=548_208, total_seqs=None, width=16, query_file="tests/golden/data/P18080.fasta"),
 }
+
+
+def read_query_file(path):
+    """First FASTA record as synthetic-alphabet codes (the product parses
+    the same text itself through init_sequence_fasta)."""
+    from libssa_amd import synthetic as syn
+    lines = open(os.path.join(ROOT, path)).read().split("\n")
+    seq = "".join(l.strip() for l in lines[1:] if not l.startswith(">")).upper()
+    return np.array([syn.AA_ORDER.index(c) for c in seq], dtype=np.uint8)
 
 
 def matrix_table(name):
@@ -176,7 +193,11 @@ def main():
         q = syn.dna_query(args.qlen, 8)
         codes, off = syn.dna_reads(args.seqs, 150, 43 + 1000 * rank, query=q, plant_every=100000)
     else:
-        q = syn.protein_query(args.qlen, 7)
+        if cfg.get("query_file"):
+            q = read_query_file(cfg["query_file"])
+            args.qlen = len(q)
+        else:
+            q = syn.protein_query(args.qlen, 7)
         codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000, sampler="lut")
     tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
     path = os.path.join(tmpdir, "db.fas")

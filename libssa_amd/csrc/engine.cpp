@@ -44,7 +44,9 @@ void DeviceDB::release() {
     if (device >= 0) (void)hipSetDevice(device);
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
-    dfree(d_work); dfree(d_order);
+    dfree(d_work); dfree(d_order); dfree(d_lscratch);
+    d_lscratch = nullptr;
+    lscratch_cap = 0;
     d_upblk = nullptr;
     upblk_cap = 0;
     d_order = nullptr;
@@ -315,7 +317,11 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     D.device = dev;
     if (!D.stream) {
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
+        check(hipStreamCreateWithFlags(&D.stream_long, hipStreamNonBlocking), "hipStreamCreate");
         for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            D.nsimd = (uint32_t)cus * 4;
     }
     const size_t E = H.meta.size();
     auto dalloc = [&](void** p, size_t bytes, const char* what) {
@@ -353,6 +359,12 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     check(hipMemcpy(D.d_lane_len, H.lane_len.data(), H.lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
     check(hipMemcpy(D.d_lane_out, H.lane_out.data(), H.lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
     D.ngroups = (uint32_t)H.groups.size();
+    D.group_ncols.resize(H.groups.size());
+    D.ncols_sum = 0;
+    for (size_t g = 0; g < H.groups.size(); g++) {
+        D.group_ncols[g] = H.groups[g].ncols;
+        D.ncols_sum += H.groups[g].ncols;
+    }
     D.nblocks = H.blocks;
     D.len_sorted = H.meta.len;
     std::sort(D.len_sorted.begin(), D.len_sorted.end());
@@ -628,6 +640,35 @@ static uint32_t sw_rel_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM)
     return (uint32_t)a;
 }
 
+// Leading (longest-first) groups that long_kernel scores instead of
+// pair_kernel.  One pair_kernel lane scores a whole entry, so a group whose
+// column count is a large part of one SIMD's share of the launch's columns
+// keeps its wave running after the rest of the chip has drained (a 548 k-entry
+// DB: 8.2 instead of 11.8 TCUPS); long_kernel spreads such an entry's query
+// rows over a wave.  Also every group holding an entry beyond the pair
+// kernel's f16 length bound (`beyond` entries, longest first).  Returns
+// UINT32_MAX when `beyond` cannot be covered; 0 when the int32 bound of
+// long_kernel does not hold or the option is off.
+static constexpr uint32_t kLongMaxGroups = 256;
+static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM) {
+    const Config& C = cfg();
+    const uint32_t need = (uint32_t)((beyond + 63) / 64);
+    if (C.long_groups == 0 || D.ngroups == 0 || D.alpha > 32) return need ? UINT32_MAX : 0;
+    const int64_t amp = std::max(std::abs(minM), std::abs(maxM)) + std::abs((int64_t)Q) + std::abs((int64_t)R);
+    if ((int64_t)(m + D.len_sorted.back() + 2) * amp >= (1ll << 30)) return need ? UINT32_MAX : 0;
+    uint32_t g = 0;
+    if (C.long_groups > 0) {
+        g = std::min<uint32_t>((uint32_t)C.long_groups, D.ngroups);
+    } else if (D.ngroups >= 2 * D.nsimd) {
+        // (a smaller DB does not fill the chip twice over: every wave starts
+        // at once and no group outlasts a drained chip)
+        const double thr = (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0;
+        while (g < D.ngroups && g < kLongMaxGroups && D.group_ncols[g] > thr) g++;
+    }
+    g = std::max(g, need);
+    return need > kLongMaxGroups ? UINT32_MAX : g;
+}
+
 bool batch_pipelinable(size_t nqueries, size_t k) {
     return nqueries > 1 && k > 0 && k <= (size_t)kFilterMaxK && !cfg().no_filter;
 }
@@ -777,15 +818,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // by the int64 kernel); otherwise the strip kernels
         uint32_t nw_base = 0;
         bool use_pair = false;
+        uint32_t long_groups = 0;            // leading groups scored by long_kernel
         if (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
             uint32_t lim = nw ? nw_f16_limit(m, Q, R, minM, maxM, &nw_base) : sw_rel_limit(m, Q, R, minM, maxM);
             lim = std::min(lim, nmax16);
             if (lim > 0) {
                 const size_t beyond = (size_t)(D.len_sorted.end() -
                                                std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
-                if (beyond <= 64) {
+                const uint32_t lg = long_plan(D, m, beyond, Q, R, minM, maxM);
+                if (lg != UINT32_MAX || beyond <= 64) {
                     use_pair = true;
                     nmax16 = lim;
+                    long_groups = lg == UINT32_MAX ? 0 : lg;
                 }
             }
         }
@@ -849,13 +893,16 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         int64_t Mc[1024];
         for (int x = 0; x < 32; x++)
             for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(D.code_of[x] << 5) + y] : -1;
+        const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
+        // a multi-view search's earlier views may still be queued on the
+        // stream: drain it before a device buffer they read is reallocated
+        if (piped && v > 0 && (D.qpt_cap < qpt_words || D.work_cap < (size_t)wide_threads * 2 * m))
+            check(hipStreamSynchronize(D.stream), "sync");
         if (D.qpt_cap < qpt_words) {
             dfree(D.d_qpt);
             check(hipMalloc((void**)&D.d_qpt, qpt_words * 4), "qpt");
             D.qpt_cap = qpt_words;
         }
-
-        const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
         if (D.work_cap < (size_t)wide_threads * 2 * m) {
             dfree(D.d_work);
             check(hipMalloc((void**)&D.d_work, (size_t)wide_threads * 2 * m * 8), "wide scratch");
@@ -885,6 +932,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // device upload block: [matrix 8 KB][top boundary][query codes]
         const size_t top_bytes = (top.size() * 4 + 15) & ~(size_t)15;
         const size_t blk_bytes = 8192 + top_bytes + m;
+        const size_t up_bytes = blk_bytes + 16 + qpt.size() * 4;
+        // the staging buffer is reused: in a multi-view search the previous
+        // view's copies may still be queued behind its predecessor's kernel
+        // (waited for before the buffer is refilled or reallocated); growing
+        // the device block drains the stream (its kernels read the old one)
+        if (piped && v > 0) {
+            if (D.upblk_cap < blk_bytes) check(hipStreamSynchronize(st), "sync");
+            else check(hipEventSynchronize(D.ev[5]), "staging");
+        }
         if (D.upblk_cap < blk_bytes) {
             dfree(D.d_upblk);
             D.upblk_cap = blk_bytes + 4096;
@@ -895,15 +951,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         D.d_query = D.d_upblk + 8192 + top_bytes;
         // one pinned staging buffer for the per-search uploads (pageable
         // sources would make each copy a synchronous staged transfer)
-        const size_t up_bytes = blk_bytes + 16 + qpt.size() * 4;
         if (D.h_up_cap < up_bytes) {
             if (D.h_up) (void)hipHostFree(D.h_up);
             check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
             D.h_up_cap = up_bytes;
         }
-        // the staging buffer is reused: in a multi-view search the previous
-        // view's copies may still be queued behind its predecessor's kernel
-        if (piped && v > 0) check(hipEventSynchronize(D.ev[5]), "staging");
         // staging mirrors the device block, then the strip kernels' table
         uint8_t* up_m = D.h_up;
         uint8_t* up_t = up_m + 8192;
@@ -988,16 +1040,50 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (v == 0) prep = now_ms() - t_prep0;
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         check(hipEventRecord(ev_k0, st), "event");
+        if (long_groups > 0) {
+            // the longest groups on the second stream, concurrently with the
+            // pair kernel (enqueued first, so their waves start first)
+            const int rl = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
+            LongArgs la{};
+            la.res = D.d_res;
+            la.groups = D.d_groups;
+            la.lane_len = D.d_lane_len;
+            la.lane_out = D.d_lane_out;
+            la.query = D.d_query;
+            la.matrix = D.d_matrix;
+            la.scores = a.scores;
+            la.nseq = long_groups * 64;
+            la.m = (uint32_t)m;
+            la.alpha = A;
+            la.gap_open = Q;
+            la.gap_extend = R;
+            if (m > (size_t)64 * rl) {
+                la.stride = D.group_ncols[0] + 16;
+                const size_t need = (size_t)la.nseq * la.stride;
+                if (D.lscratch_cap < need) {
+                    check(hipStreamSynchronize(D.stream_long), "sync");
+                    dfree(D.d_lscratch);
+                    check(hipMalloc((void**)&D.d_lscratch, need * 8), "long-entry scratch");
+                    D.lscratch_cap = need;
+                }
+                la.scratch = D.d_lscratch;
+            }
+            check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
+            check(launch_long(la, rl, nw, D.stream_long), "long kernel launch");
+            check(hipEventRecord(D.ev[7], D.stream_long), "event");
+        }
         if (use_pair) {
             StripArgs b = a;
             b.nstrips = main_strips;
             b.qpt_tail = D.d_qpt + tail_off;
             b.top = (const uint4*)D.d_top;
+            b.g_first = long_groups;
             const int lnp = main_strips ? pnp : tail_np;
             check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
+        if (long_groups > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
         check(hipEventRecord(ev_k1, st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;

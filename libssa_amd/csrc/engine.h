@@ -76,6 +76,15 @@ struct DeviceDB {
     int64_t* d_matrix = nullptr;
     int64_t* d_work = nullptr;
     size_t work_cap = 0;
+    // long entries (long_kernel, launched on stream_long beside the pair
+    // kernel): the groups' column counts (longest first), their sum, the
+    // device's SIMD count, the multi-pass scratch
+    std::vector<uint32_t> group_ncols;
+    uint64_t ncols_sum = 0;
+    uint32_t nsimd = 1024;
+    hipStream_t stream_long = nullptr;
+    int64_t* d_lscratch = nullptr;
+    size_t lscratch_cap = 0;              // int64 elements
     std::vector<uint32_t> lane_out;       // host copy for overflow mapping
     std::vector<uint32_t> len_sorted;     // entry lengths, ascending
     // residues are stored in a compact alphabet: device code c < alpha stands

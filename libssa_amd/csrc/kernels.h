@@ -38,7 +38,30 @@ struct StripArgs {
     // as diagonal-relative patterns in row-buffer quads, the same for every
     // lane ([ceil(max ncols / 4)] uint4)
     const uint4* top;
+    // pair_kernel: first group it scores (groups before it go to long_kernel)
+    uint32_t g_first;
 };
+
+// Long DB entries (long_kernel): one wave per entry, the query rows split over
+// the 64 lanes (RL consecutive rows per lane, passes of 64*RL rows), DB
+// columns swept as a lane-skewed wavefront; exact int32 arithmetic.  Serves
+// the entries of the first nseq/64 (longest) groups, which pair_kernel then
+// skips (StripArgs::g_first).
+struct LongArgs {
+    const uint4* res;
+    const GroupDesc* groups;
+    const uint32_t* lane_len;
+    const uint32_t* lane_out;
+    const uint8_t* query;      // [m]
+    const int64_t* matrix;     // [1024] compact code x query code
+    int32_t* scores;
+    int64_t* scratch;          // [nseq][stride] (H, F) of a pass's last row (multi-pass only)
+    uint32_t stride;
+    uint32_t nseq;             // entries served: lanes [0, nseq) of the group order
+    uint32_t m, alpha;
+    int32_t gap_open, gap_extend;
+};
+constexpr int kLongWaves = 4;
 
 struct WideArgs {
     const uint4* res;
@@ -92,6 +115,9 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 // required for NW, whose score is captured in the last strip)
 hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
+// rl: rows per lane (4, 8, 12 or 16; 64*rl rows per pass)
+hipError_t launch_long(const LongArgs& a, int rl, bool nw, hipStream_t st);
+size_t long_lds_bytes(uint32_t alpha, int rl);
 
 // pair_kernel's per-search pair tables, built on the device from the query
 // and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)

@@ -500,9 +500,9 @@ pair_kernel(const StripArgs a) {
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t g = blockIdx.x * W + wave;
+    const uint32_t g = a.g_first + blockIdx.x * W + wave;
     const bool active = g < a.ngroups;
-    const uint32_t gg = active ? g : 0;
+    const uint32_t gg = active ? g : a.g_first;
 
     const GroupDesc gd = a.groups[gg];
     const uint32_t nquads = gd.ncols >> 2;
@@ -1077,6 +1077,193 @@ hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ long entries
+// One wave per DB entry of the longest groups, so that a handful of entries
+// far longer than the rest no longer set the launch's duration (one lane of
+// pair_kernel scores a whole entry: its wave runs ncols x strips steps while
+// the rest of the chip has drained).  The query's rows are split over the
+// lanes -- lane l holds rows i0p + l*RL .. + RL-1 of pass p (64*RL rows per
+// pass) -- and the entry's columns sweep through the lanes as a skewed
+// wavefront: at step t lane l scores column j = t - l of its rows, taking H
+// and F of the row above (lane l-1's last row at column j, made at step t-1)
+// and the residue through a one-lane DPP shift.  The recurrences are the
+// reference's 64-bit scorers (smith_waterman_63.c:32-98,
+// needleman_wunsch_64.c:32-98; oracle_full_sw / oracle_full_nw), in int32,
+// exact under the host's bound (engine.cpp).  A pass's last row is kept in
+// scratch for the next pass's lane 0.
+__device__ __forceinline__ int32_t shr1(int32_t lane0_value, int32_t v) {
+    // DPP wave_shr:1 -- lane l receives lane l-1's v, lane 0 keeps lane0_value
+    return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138, 0xf, 0xf, false);
+}
+
+template <int RL, bool NW>
+__global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int16_t ltab[];
+    constexpr uint32_t RP = 64 * RL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t s = blockIdx.x * kLongWaves + wave;
+    const bool active = s < a.nseq;
+    const uint32_t ss = active ? s : 0;
+    const GroupDesc gd = a.groups[ss >> 6];
+    const uint32_t n = a.lane_len[ss];
+    const uint4* rp = a.res + (size_t)gd.blk * 64 + (ss & 63);
+    int64_t* scr = a.scratch + (size_t)ss * a.stride;
+    const int32_t Q = a.gap_open, R = a.gap_extend, QR = Q + R;
+    const uint32_t m = a.m, prow = a.alpha + 1;
+    const uint32_t npass = (m + RP - 1) / RP;
+    int32_t S = 0, score = 0;
+    for (uint32_t p = 0; p < npass; p++) {
+        const uint32_t i0p = p * RP;
+        // the pass's profile [code][row] (padding code and rows: -4096); the
+        // fence orders the previous pass's scratch stores before its loads
+        __threadfence();
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < prow * RP; t += 64 * kLongWaves) {
+            const uint32_t c = t / RP, i = i0p + t % RP;
+            ltab[t] = (c < a.alpha && i < m) ? (int16_t)a.matrix[(c << 5) + a.query[i]] : (int16_t)-4096;
+        }
+        __syncthreads();
+        if (!active || n == 0) continue;
+        const bool lastp = p + 1 == npass;
+        const int i0 = (int)(i0p + lane * RL);
+        const int lmax = (int)((min(m - i0p, RP) - 1) / RL);   // last lane holding query rows
+        // left boundary: H(i, -1) and E into column 0
+        int32_t H[RL], E[RL];
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            H[r] = NW ? Q + (i0 + r + 1) * R : 0;
+            E[r] = NW ? 2 * Q + (i0 + r + 2) * R : 0;
+        }
+        int32_t hdiag = NW ? (i0 == 0 ? 0 : Q + i0 * R) : 0;   // H(i0-1, -1)
+        int32_t hbot = 0, fbot = 0;
+        uint32_t d = 0;
+        // residues and (later passes) the previous pass's last row are
+        // fetched a 16-column block ahead; the row is lane-distributed (lane
+        // k holds column 16b + (k & 15)) and read back with v_readlane
+        uint4 blk = rp[0], blk_next = n > 16 ? rp[64] : make_uint4(0, 0, 0, 0);
+        auto scr_load = [&](uint32_t c) -> int64_t {
+            return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        };
+        int64_t row = 0, row_next = 0;
+        if (p > 0) {
+            row = scr_load(lane & 15);
+            row_next = scr_load(16 + (lane & 15));
+        }
+        const uint32_t steps = n + (uint32_t)lmax;
+        for (uint32_t t = 0; t < steps; t++) {
+            // lane 0's inputs at column t: the top boundary H(-1, t), F into
+            // row 0 (first pass), or the previous pass's last row
+            int32_t th = 0, tf = 0;
+            uint32_t dn = 0;
+            if (t < n) {
+                if ((t & 15) == 0 && t > 0) {
+                    blk = blk_next;
+                    if (t + 16 < n) blk_next = rp[(size_t)((t >> 4) + 1) * 64];
+                    if (p > 0) {
+                        row = row_next;
+                        row_next = scr_load(t + 16 + (lane & 15));
+                    }
+                }
+                if (p == 0) {
+                    if (NW) {
+                        th = Q + ((int32_t)t + 1) * R;
+                        tf = 2 * Q + ((int32_t)t + 2) * R;
+                    }
+                } else {
+                    th = __builtin_amdgcn_readlane((int32_t)row, t & 15);
+                    tf = __builtin_amdgcn_readlane((int32_t)(row >> 32), t & 15);
+                }
+                const uint32_t w = (t & 8) ? ((t & 4) ? blk.w : blk.z) : ((t & 4) ? blk.y : blk.x);
+                dn = (w >> (8 * (t & 3))) & 0xffu;
+            }
+            const int32_t hin = shr1(th, hbot);
+            const int32_t fin = shr1(tf, fbot);
+            d = (uint32_t)shr1((int32_t)dn, (int32_t)d);
+            const int j = (int)t - lane;
+            if (lane <= lmax && j >= 0 && j < (int)n) {
+                const uint2* pp = (const uint2*)(ltab + d * RP + lane * RL);
+                int32_t P[RL];
+#pragma unroll
+                for (int q = 0; q < RL / 4; q++) {
+                    const uint2 v = pp[q];
+                    P[4 * q] = (int32_t)(int16_t)(v.x & 0xffffu);
+                    P[4 * q + 1] = (int32_t)v.x >> 16;
+                    P[4 * q + 2] = (int32_t)(int16_t)(v.y & 0xffffu);
+                    P[4 * q + 3] = (int32_t)v.y >> 16;
+                }
+                int32_t hd = hdiag, f = fin;
+#pragma unroll
+                for (int r = 0; r < RL; r++) {
+                    const int32_t up = H[r];
+                    int32_t h = max(max(hd + P[r], E[r]), f);
+                    if (!NW) {
+                        h = max(h, 0);
+                        S = max(S, h);
+                    }
+                    H[r] = h;
+                    const int32_t tt = h + QR;
+                    E[r] = max(E[r] + R, tt);
+                    f = max(f + R, tt);
+                    hd = up;
+                }
+                hdiag = hin;
+                hbot = H[RL - 1];
+                fbot = f;
+                if (!lastp && lane == 63)
+                    __hip_atomic_store(scr + j, (int64_t)(uint32_t)hbot | ((int64_t)fbot << 32), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (NW && lastp) {
+            // H(m-1, n-1): the lane holding row m-1 stopped updating after
+            // column n-1
+            const uint32_t rr = m - 1 - i0p;
+            int32_t hs = H[0];
+#pragma unroll
+            for (int r = 1; r < RL; r++) hs = (rr % RL == (uint32_t)r) ? H[r] : hs;
+            score = __builtin_amdgcn_readlane(hs, rr / RL);
+        }
+    }
+    if (!active) return;
+    const uint32_t o = a.lane_out[ss];
+    if (o == 0xffffffffu) return;
+    if (!NW) {
+        for (int x = 32; x > 0; x >>= 1) S = max(S, __shfl_xor(S, x));
+        score = S;
+    }
+    if (n == 0) score = NW ? Q + (int32_t)m * R : 0;
+    if (lane == 0) a.scores[o] = score;
+}
+
+size_t long_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * rl * 2; }
+
+template <int RL, bool NW>
+static hipError_t launch_long_t(const LongArgs& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)long_kernel<RL, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)long_lds_bytes(32, 16));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
+    hipLaunchKernelGGL((long_kernel<RL, NW>), dim3(blocks), dim3(64 * kLongWaves), long_lds_bytes(a.alpha, RL), st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_long(const LongArgs& a, int rl, bool nw, hipStream_t st) {
+    if (a.nseq == 0) return hipSuccess;
+    if (a.alpha > 32) return hipErrorInvalidValue;
+    switch (rl) {
+        case 4: return nw ? launch_long_t<4, true>(a, st) : launch_long_t<4, false>(a, st);
+        case 8: return nw ? launch_long_t<8, true>(a, st) : launch_long_t<8, false>(a, st);
+        case 12: return nw ? launch_long_t<12, true>(a, st) : launch_long_t<12, false>(a, st);
+        case 16: return nw ? launch_long_t<16, true>(a, st) : launch_long_t<16, false>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 // ------------------------------------------------------------------ launch
 template <int NP, bool NW>
 static hipError_t launch_np(const StripArgs& a, hipStream_t st) {
@@ -1111,7 +1298,7 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
         attr = true;
     }
     constexpr int W = pair_waves(NP, NW);
-    const uint32_t blocks = (a.ngroups + W - 1) / W;
+    const uint32_t blocks = (a.ngroups - a.g_first + W - 1) / W;
     hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }
@@ -1128,7 +1315,7 @@ static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, 
 }
 
 hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st) {
-    if (a.ngroups == 0 || (a.nstrips == 0 && npt == 0)) return hipSuccess;
+    if (a.ngroups <= a.g_first || (a.nstrips == 0 && npt == 0)) return hipSuccess;
     // NW scores come from the tail strip's capture
     if (nw && npt == 0) return hipErrorInvalidValue;
     if (np == 24) return nw ? launch_pair_np<24, true>(a, npt, lds_bytes, st) : launch_pair_np<24, false>(a, npt, lds_bytes, st);

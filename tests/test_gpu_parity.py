@@ -153,6 +153,43 @@ def test_query_length_edges_vs_oracle(qlen, algo):
         S.free_sequence(qq)
 
 
+@pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_long_entry_kernel_vs_oracle(qlen, algo):
+    """long_kernel (one wave per entry, query rows over the lanes, passes of
+    up to 1024 rows) on the leading (longest) groups -- forced to 1 and 3 of
+    the 4 groups, and to none -- gives every entry the oracle's score; the
+    DB has entries of 1..4100 residues, empty records and a planted copy of
+    the query."""
+    rng = np.random.default_rng(1000 + qlen)
+    q = syn.protein_query(qlen, 200 + qlen)
+    lens = np.array([3000, 1, 0, 2500, 17, 64, 4100, qlen + 7] + list(rng.integers(1, 400, 248)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    codes[int(off[7]) + 3:int(off[7]) + 3 + qlen] = q           # high-scoring entry
+    codes[int(off[6]) + 100:int(off[6]) + 100 + qlen] = q       # inside the longest one
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            for lg in (1, 3, 0):
+                S.set_option("long_groups", lg)
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all()
+                assert (sc == exp).all(), (lg, np.nonzero(sc != exp)[0][:10])
+                got = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
+                assert got == po.topk(exp, keep.astype(np.uint64), 10)
+        finally:
+            S.set_option("long_groups", -1)
+        S.free_sequence(qq)
+
+
 @pytest.mark.parametrize("match", [40, 55, 127])
 def test_sw_f16_pattern_limit(match):
     """Scores around the f16-pattern kernel's exact range (29695) and the
@@ -182,8 +219,10 @@ def test_nw_f16_length_bound(n_long):
     """NW on f16 patterns admits entries up to a length bound derived from the
     query, matrix and gaps (engine.cpp nw_f16_limit): with R=-30 and a
     100-residue query it is 874, the int16 bound 984.  Lengths straddle both;
-    a few long entries are re-scored exactly, many long ones switch the whole
-    search to the int16 kernel -- every score stays exact either way."""
+    by default the groups holding entries beyond the bound go to long_kernel
+    (exact int32, nothing left for the int64 re-score); without it a few long
+    entries are re-scored exactly, many long ones switch the whole search to
+    the int16 kernel -- every score stays exact either way."""
     rng = np.random.default_rng(n_long)
     q = syn.protein_query(100, 11)
     lens = np.concatenate([np.arange(860, 890), [980, 984, 985, 990, 1200],
@@ -197,12 +236,19 @@ def test_nw_f16_length_bound(n_long):
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
-        for swk in (0, 1):
-            S.set_option("sw_kernel", swk)
-            sc, _ = _full_scores(qq, S.NW, len(lens))
-            assert (sc == exp).all(), (swk, np.nonzero(sc != exp)[0][:10])
-            assert S.stats()["wide_count"] >= 2
-        S.set_option("sw_kernel", 0)
+        try:
+            for swk, lg in ((0, -1), (0, 0), (1, -1)):
+                S.set_option("sw_kernel", swk)
+                S.set_option("long_groups", lg)
+                sc, _ = _full_scores(qq, S.NW, len(lens))
+                assert (sc == exp).all(), (swk, lg, np.nonzero(sc != exp)[0][:10])
+                if (swk, lg) == (0, -1):
+                    assert S.stats()["kernel"] == "pair_f16_nw" and S.stats()["wide_count"] == 0
+                else:
+                    assert S.stats()["wide_count"] >= 2
+        finally:
+            S.set_option("sw_kernel", 0)
+            S.set_option("long_groups", -1)
         S.free_sequence(qq)
 
 
@@ -269,9 +315,17 @@ def test_int16_overflow_reroute(algo):
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(base))
-        sc, _ = _full_scores(qq, algo, 4)
-        assert (sc == exp).all()
-        assert S.stats()["wide_count"] >= 1
+        try:
+            # by default the entries beyond the f16 bound go to long_kernel
+            # (int32); without it through the overflow list
+            for lg in (-1, 0):
+                S.set_option("long_groups", lg)
+                sc, _ = _full_scores(qq, algo, 4)
+                assert (sc == exp).all(), lg
+                if lg == 0:
+                    assert S.stats()["wide_count"] >= 1
+        finally:
+            S.set_option("long_groups", -1)
         S.free_sequence(qq)
 
 
@@ -714,6 +768,58 @@ def test_full_size_config_properties(cfg, tmp_path):
     fn = S.sw_align if algo == S.SW else S.nw_align
     for k in (1, 10, 64):
         assert [(h["score"], h["id"]) for h in fn(qq, k, 16)] == po.topk(sc, ids, k)
+    S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("cfg", ["c5", "ref"])
+def test_other_config_properties(cfg, tmp_path):
+    """The other bench shapes, scaled to a few seconds: C5 (DNA reads of 150
+    nt, constant +5/-4, gaps -4/-2; a 2000-nt query instead of 10 k, 200 k
+    reads instead of 50 M) and the reference's published benchmark shape
+    (P18080, BLOSUM50, gaps -3/-1; 100 k synthetic sequences).  Same
+    properties as above: default kernel == int16 strip kernel on every score,
+    oracle int64 on a sample + the top hits, device top-k == host replay."""
+    if cfg == "c5":
+        algo, go, ge, nuc = S.SW, -4, -2, True
+        q = syn.dna_query(2000, 8)
+        codes, off = syn.dna_reads(200_000, 150, 43, query=q, plant_every=10000)
+        configure(True, ("const", 5, -4), go, ge)
+        M = po.matrix_constant(5, -4)
+    else:
+        algo, go, ge, nuc = S.SW, -3, -1, False
+        text = open(os.path.join(DATA, "P18080.fasta")).read().split("\n")
+        seq = "".join(l.strip() for l in text[1:] if not l.startswith(">")).upper()
+        q = np.array([syn.AA_ORDER.index(c) for c in seq], dtype=np.uint8)
+        codes, off = syn.protein_db(100_000, 44, query=q, plant_every=5000, sampler="lut")
+        configure(False, ("builtin", "blosum50"), go, ge)
+        M = TABLES["matrices"][NAMES.index("blosum50")].copy()
+    path = str(tmp_path / "db.fas")
+    syn.write_fasta(path, codes, off, nucleotide=nuc)
+    S.init_db(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=nuc))
+    n = len(off) - 1
+    vecs = {}
+    for swk in (0, 1):
+        S.set_option("sw_kernel", swk)
+        log = S.search(qq, algo, n + 1, 16, S.LOG, cap=n + 8)
+        assert len(log) == n
+        vecs[swk] = np.array([h[0] for h in log], np.int64)
+        if swk == 1:
+            assert S.stats()["kernel"] == "strip16_sw"
+        elif cfg == "c5":
+            assert S.stats()["kernel"] == "pair_f16_sw"
+    S.set_option("sw_kernel", 0)
+    assert (vecs[0] == vecs[1]).all(), np.nonzero(vecs[0] != vecs[1])[0][:10]
+    sc = vecs[0]
+    rng = np.random.default_rng(98)
+    top = np.argsort(-sc, kind="stable")[:50]
+    sample = np.unique(np.concatenate([rng.choice(n, 300, replace=False), top]))
+    seqs = [codes[int(off[i]):int(off[i + 1])] for i in sample]
+    db, soff = po.pack_db(seqs)
+    assert (po.scores(algo, q, db, soff, M, go, ge) == sc[sample]).all()
+    ids = np.arange(n, dtype=np.uint64)
+    for k in (1, 10, 64):
+        assert [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)] == po.topk(sc, ids, k)
     S.free_sequence(qq)
 
 
