@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--long-tail", type=int, default=0,
+                   help="replace N DB sequences by 5k-35k-residue ones (a UniProt-like length tail)")
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
     p.add_argument("--pair-np", type=int, default=24, help="pair kernel main strip: 24 (48 rows) or 16 (32 rows)")
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
@@ -199,6 +201,23 @@ def main():
         else:
             q = syn.protein_query(args.qlen, 7)
         codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000, sampler="lut")
+        if args.long_tail > 0:
+            # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
+            # residues); the others keep theirs
+            rng = np.random.default_rng(77 + rank)
+            lens = np.diff(off).astype(np.int64)
+            tail = np.zeros(args.seqs, bool)
+            tail[np.arange(args.long_tail) * (args.seqs // args.long_tail)] = True
+            lens[tail] = rng.integers(5000, 35001, int(tail.sum()))
+            noff = np.zeros(args.seqs + 1, np.uint64)
+            np.cumsum(lens, out=noff[1:])
+            seg = np.repeat(np.arange(args.seqs), lens)
+            src = off[seg].astype(np.int64) + (np.arange(len(seg)) - noff[seg].astype(np.int64))
+            ncodes = syn._aa_lut()[rng.integers(0, 65536, size=len(seg), dtype=np.uint16)]
+            keep = ~tail[seg]
+            ncodes[keep] = codes[src[keep]]
+            codes, off = ncodes, noff
+            del seg, src, keep
     tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
     path = os.path.join(tmpdir, "db.fas")
     syn.write_fasta(path, codes, off, nucleotide=dna)

@@ -662,6 +662,9 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
     } else if (D.ngroups >= 2 * D.nsimd) {
         // (a smaller DB does not fill the chip twice over: every wave starts
         // at once and no group outlasts a drained chip)
+        // (a lower threshold costs more than it gains: long_kernel's cost per
+        // cell is several times pair_kernel's -- the 548 k-entry DB: 40 %
+        // 9.7, 50 % 10.9, 65 % 10.9 TCUPS)
         const double thr = (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0;
         while (g < D.ngroups && g < kLongMaxGroups && D.group_ncols[g] > thr) g++;
     }

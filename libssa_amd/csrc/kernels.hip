@@ -1100,6 +1100,9 @@ template <int RL, bool NW>
 __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
     extern __shared__ __attribute__((aligned(16))) int16_t ltab[];
     constexpr uint32_t RP = 64 * RL;
+    // these waves are the launch's critical path: they issue before the
+    // pair kernel's waves sharing their SIMD
+    __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t s = blockIdx.x * kLongWaves + wave;

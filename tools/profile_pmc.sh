@@ -17,7 +17,7 @@ PASSES=${PASSES:-"stats fetch write valu wait lds icache"}
 run() {   # name, rocprof args...
     local name=$1; shift
     case " $PASSES " in *" $name "*) ;; *) return 0 ;; esac
-    timeout -k 10 300 rocprofv3 "$@" --kernel-include-regex "strip|pair" -d "$OUT/$name" -o run --output-format csv \
+    timeout -k 10 300 rocprofv3 "$@" --kernel-include-regex "strip|pair|long" -d "$OUT/$name" -o run --output-format csv \
         -- python3 "$REPO/bench.py" $ARGS > "$OUT/$name.log" 2>&1
 }
 run stats --kernel-trace --stats
