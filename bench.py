@@ -45,9 +45,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # pmc_c3_r01b (32-row pair strips), pmc_c2_np24 / pmc_c3_np24 (48-row strips),
 # pmc_c2_rel / pmc_c3_rel (48-row strips, diagonal-relative values),
 # pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals),
-# pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory: the
+# pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory),
+# pmc_{c2,c3,c5,ref}_r01g (+ diagonal add as v_add_u32, long_kernel: the
 # default, these values)
 VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 3.05, "pair_f16_nw": 2.74}
+# share of those that are full-rate v_add_u32 (2.5 cycles per wave64
+# instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
+# profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
+# (tools/hotloop.py: per 48-row column SW 49 of 142.8, NW 49 of 128.8)
+VALU_FAST_SHARE = {"pair_f16_sw": 0.343, "pair_f16_nw": 0.380}
 
 
 def parse():
@@ -287,12 +293,13 @@ def main():
         rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_pair{args.pair_np}")
         if rec:
             traffic = rec["bytes_per_launch"]
-    # VALU issue roofline: the strip kernel is made of
-    # half-rate VOP3/VOP3P instructions (4.17 cycles per wave64 instruction
-    # per SIMD, measured: profiles/r01/ubench_valu_rates2.txt); instructions
-    # per cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01e).
+    # VALU issue roofline: VOP3/VOP3P instructions issue at
+    # 4.17 cycles per wave64 instruction per SIMD, v_add_u32 at 2.5 (measured
+    # in isolation: profiles/r01/ubench_valu_rates4.txt); instructions per
+    # cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01g).
     instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 and args.pair_np == 24 else None
-    issue_cycles = 4.17
+    fast = VALU_FAST_SHARE.get(st["kernel"], 0.0)
+    issue_cycles = (1.0 - fast) * 4.17 + fast * 2.5
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
         "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
