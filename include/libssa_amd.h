@@ -73,6 +73,15 @@ void ssa_amd_set_id_offset( size_t offset );
 int ssa_amd_set_devices( const int * devices, int n );
 int ssa_amd_prepare_db( void );            /* pack + upload the DB now; returns 0 on success */
 void ssa_amd_get_stats( ssa_amd_stats_t * out );
+/* Tuning knobs (results never change, only which kernel computes them):
+ *   "strip_np" 8|16|32   int16 strip kernels: packed rows per strip
+ *   "pair_np" 16|24      pair kernel main strip (32 / 48 rows)
+ *   "sw_kernel" 0|1      1: int16 strip kernel instead of the pair kernel
+ *   "force_wide" 0|1     1: every entry through the int64 kernel
+ *   "no_filter" 0|1      1: copy every score back (no device top-k filter)
+ *   "long_groups" -1|0|N leading groups scored one entry per wave: auto, never, N
+ *   "long_share_pct" P   auto threshold: P % of one SIMD's share of all columns
+ * Unknown names print a warning. */
 void ssa_amd_set_option( const char * name, long value );
 
 /* Scores the open DB against the query.  mode: SSA_AMD_TOPK or SSA_AMD_LOG.
