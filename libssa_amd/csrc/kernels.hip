@@ -1199,15 +1199,15 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
 #pragma unroll
                 for (int r = 0; r < RL; r++) {
                     const int32_t up = H[r];
-                    int32_t h = max(max(hd + P[r], E[r]), f);
-                    if (!NW) {
-                        h = max(h, 0);
-                        S = max(S, h);
-                    }
+                    // SW keeps E and F clamped at 0, which makes h >= 0 with
+                    // no extra max: exact for R <= 0 (max(E,0) + R <= 0
+                    // wherever E < 0, so every max(., 0) downstream agrees)
+                    const int32_t h = max(max(hd + P[r], E[r]), f);
+                    if (!NW) S = max(S, h);
                     H[r] = h;
                     const int32_t tt = h + QR;
-                    E[r] = max(E[r] + R, tt);
-                    f = max(f + R, tt);
+                    E[r] = NW ? max(E[r] + R, tt) : max(max(E[r] + R, tt), 0);
+                    f = NW ? max(f + R, tt) : max(max(f + R, tt), 0);
                     hd = up;
                 }
                 hdiag = hin;
