@@ -86,6 +86,117 @@ def protein_db(n: int, seed: int = 42, query: np.ndarray | None = None, plant_ev
     return codes, off
 
 
+# --------------------------------------------------------------------------
+# Block-seeded generators: sequence ID range [i0, i1) of an n-sequence DB,
+# generated without the rest of it.  Block b (BLOCK consecutive IDs) draws
+# from its own PCG64(SeedSequence([seed, b])) stream, so a rank's shard is
+# byte-identical to the same slice of the whole DB: a strong-scaling run at
+# N = 1/2/4/8 GPUs searches one and the same DB (bench.py c4/c5), and a test
+# can regenerate any share of a 10 M-sequence DB in seconds.
+# --------------------------------------------------------------------------
+BLOCK = 1 << 16
+
+# Residue sets (amino-acid codes of AA_ORDER) and their frequencies:
+#   bg20      the 20 standard residues, BLOSUM62 background frequencies;
+#   sprot25   + X, B, Z, U, O at roughly UniProtKB/Swiss-Prot's (tiny) rates,
+#             i.e. the 25 symbols util_sequence.c:36-44 maps for a real DB;
+#   uniform28 the reference's own DB generator: every one of the 28 symbols
+#             of "-ABCDEFGHIKLMNPQRSTVWXYZU*OJ" equally likely
+#             (benchmark/src/generate_db.c:117-120; '-' is unknown to the
+#             provider and becomes code 0, util_sequence.c:303-309).
+# (each at least two of the 65536 slots of the sampling table)
+_RARE25 = {"X": 2e-4, "B": 5e-5, "Z": 5e-5, "U": 3.1e-5, "O": 3.1e-5}
+
+
+def alphabet_table(alphabet: str) -> tuple[np.ndarray, np.ndarray]:
+    if alphabet == "bg20":
+        return AA_CODES, AA_PROBS
+    if alphabet == "sprot25":
+        codes = np.concatenate([AA_CODES, [AA_ORDER.index(c) for c in _RARE25]]).astype(np.uint8)
+        probs = np.concatenate([AA_PROBS * (1.0 - sum(_RARE25.values())), list(_RARE25.values())])
+        return codes, probs / probs.sum()
+    if alphabet == "uniform28":
+        return np.arange(28, dtype=np.uint8), np.full(28, 1.0 / 28)
+    raise ValueError(f"unknown alphabet {alphabet}")
+
+
+def _lut(codes: np.ndarray, probs: np.ndarray) -> np.ndarray:
+    cdf = np.cumsum(probs)
+    u = (np.arange(65536) + 0.5) / 65536.0
+    return codes[np.minimum(np.searchsorted(cdf, u), len(codes) - 1)].astype(np.uint8)
+
+
+def protein_db_range(n: int, seed: int, i0: int = 0, i1: int | None = None, query: np.ndarray | None = None,
+                     plant_every: int = 10000, lo: int = 16, hi: int = 4096, alphabet: str = "bg20",
+                     lengths: str = "gamma"):
+    """Sequences [i0, i1) of the block-seeded n-sequence protein DB:
+    (codes uint8[total], offsets uint64[i1 - i0 + 1]).
+
+    lengths "gamma": 1 + round(Gamma(2, 175)) clipped to [lo, hi] (SURVEY.md
+    §8d); "uniform": uniform in [lo, hi) like generate_db.c:109-112.  A mutated
+    copy of the query (30-95 % identity, short indels) replaces every
+    sequence whose ID is plant_every/2 modulo plant_every."""
+    i1 = n if i1 is None else min(i1, n)
+    if not 0 <= i0 <= i1:
+        raise ValueError("bad ID range")
+    codes_a, probs_a = alphabet_table(alphabet)
+    lut = _lut(codes_a, probs_a)
+    parts, lens_all = [], []
+    for b in range(i0 // BLOCK, (i1 + BLOCK - 1) // BLOCK if i1 > i0 else i0 // BLOCK):
+        b0, b1 = b * BLOCK, min(n, (b + 1) * BLOCK)
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
+        if lengths == "gamma":
+            lens = np.clip(1 + np.rint(rng.gamma(2.0, 175.0, size=b1 - b0)), lo, hi).astype(np.int64)
+        else:
+            lens = rng.integers(lo, hi, size=b1 - b0).astype(np.int64)
+        plants = []
+        if query is not None and plant_every > 0:
+            prng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b, 1])))
+            first = b0 + ((plant_every // 2 - b0) % plant_every)
+            for pos in range(first, b1, plant_every):
+                hom = _mutate(prng, query)
+                lens[pos - b0] = len(hom)
+                plants.append((pos - b0, hom))
+        off = np.zeros(b1 - b0 + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        codes = lut[rng.integers(0, 65536, size=int(off[-1]), dtype=np.uint16)]
+        for pos, hom in plants:
+            codes[off[pos]:off[pos + 1]] = hom
+        s0, s1 = max(i0, b0) - b0, min(i1, b1) - b0
+        parts.append(codes[off[s0]:off[s1]])
+        lens_all.append(lens[s0:s1])
+    lens = np.concatenate(lens_all) if lens_all else np.zeros(0, np.int64)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return codes, off
+
+
+def dna_reads_range(n: int, seed: int, i0: int = 0, i1: int | None = None, length: int = 150,
+                    query: np.ndarray | None = None, plant_every: int = 100000):
+    """Reads [i0, i1) of the block-seeded n-read DNA DB (i.i.d. ACGT; every
+    read whose ID is 0 modulo plant_every is a query substring with 0-10 %
+    substitutions)."""
+    i1 = n if i1 is None else min(i1, n)
+    parts = []
+    for b in range(i0 // BLOCK, (i1 + BLOCK - 1) // BLOCK if i1 > i0 else i0 // BLOCK):
+        b0, b1 = b * BLOCK, min(n, (b + 1) * BLOCK)
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
+        codes = NT_ACGT[rng.integers(0, 4, size=(b1 - b0) * length, dtype=np.uint8)]
+        if query is not None and len(query) >= length and plant_every > 0:
+            for pos in range(b0 + (-b0 % plant_every), b1, plant_every):
+                start = int(rng.integers(0, len(query) - length + 1))
+                read = query[start:start + length].copy()
+                sub = rng.random(length) < rng.uniform(0.0, 0.10)
+                read[sub] = NT_ACGT[rng.integers(0, 4, size=int(sub.sum()))]
+                codes[(pos - b0) * length:(pos - b0 + 1) * length] = read
+        s0, s1 = max(i0, b0) - b0, min(i1, b1) - b0
+        parts.append(codes[s0 * length:s1 * length])
+    codes = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    off = np.arange(max(i1 - i0, 0) + 1, dtype=np.uint64) * np.uint64(length)
+    return codes, off
+
+
 def dna_query(length: int = 10000, seed: int = 8) -> np.ndarray:
     rng = np.random.Generator(np.random.PCG64(seed))
     return rng.choice(NT_ACGT, size=length).astype(np.uint8)

@@ -58,6 +58,12 @@ def lib():
         L.oracle_matrix_parse.argtypes = [ctypes.c_char_p, P]
         L.oracle_matrix_constant.argtypes = [ctypes.c_int, ctypes.c_int, P]
         L.oracle_build_map.argtypes = [ctypes.c_int, P]
+        L.oracle_nw_overflow.argtypes = [ctypes.c_int, P, ctypes.c_size_t, P, ctypes.c_size_t, P,
+                                         ctypes.c_int, ctypes.c_int, P]
+        L.oracle_nw_overflow.restype = ctypes.c_int
+        L.oracle_overflow_flags.argtypes = [ctypes.c_int, P, P, ctypes.c_size_t, P, ctypes.c_size_t, P,
+                                            ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
+        L.oracle_overflow_counts.argtypes = [ctypes.c_int, P, ctypes.c_size_t, ctypes.c_size_t, P]
         _lib = L
     return _lib
 
@@ -150,6 +156,30 @@ def scores(algo: int, query: np.ndarray, db: np.ndarray, off: np.ndarray, matrix
     return out[:n]
 
 
+def overflow_flags(algo: int, query: np.ndarray, db: np.ndarray, off: np.ndarray, matrix: np.ndarray,
+                   gap_open: int, gap_extend: int, threads: int = 8) -> np.ndarray:
+    """Per DB sequence: bit 0 = the reference's 8-bit kernel overflows, bit 1
+    = its 16-bit kernel does (SW: score rule; NW: saturated replay,
+    oracle_nw_overflow).  Empty sequences / query: 0."""
+    n = len(off) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    qlen = len(q)
+    if q.size == 0:
+        q = np.zeros(1, dtype=np.uint8)
+    lib().oracle_overflow_flags(algo, _ptr(db), _ptr(off), n, _ptr(q), qlen, _ptr(matrix),
+                                gap_open, gap_extend, _ptr(out), threads)
+    return out[:n]
+
+
+def overflow_counts(width: int, flags: np.ndarray) -> tuple[int, int]:
+    """(overflow_8, overflow_16) of a search from [views][seqs] flags."""
+    f = np.ascontiguousarray(np.atleast_2d(flags), dtype=np.uint8)
+    out = np.zeros(2, dtype=np.uint64)
+    lib().oracle_overflow_counts(width, _ptr(f), f.shape[0], f.shape[1], _ptr(out))
+    return int(out[0]), int(out[1])
+
+
 def topk(sc: np.ndarray, ids: np.ndarray, k: int) -> list[tuple[int, int]]:
     """Reference min-heap replay in the given insertion order, sorted
     score desc / id desc."""
@@ -189,13 +219,22 @@ def have_ref() -> bool:
 
 MODE_SCORES, MODE_SEARCH64, MODE_SEARCH16_AVX2, MODE_SEARCH16_SSE2, MODE_TABLES, MODE_TRANSLATE = 0, 1, 2, 3, 4, 5
 MODE_ALIGN = 6
+MODE_SEARCH8_AVX2 = 7
 
 
 def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_open: int = 0,
             gap_extend: int = 0, k: int = 10, chunk: int = 1000, threads: int = 1, repeat: int = 1,
-            db_off=None):
+            db_off=None, views=None, chunk_counts=False):
     """Runs the reference harness.  Returns raw per-seq scores (mode 0), the
-    tables blob (mode 4), or (hits, overflow_count, nseq, seconds)."""
+    tables blob (mode 4), or (hits, overflow_count, nseq, seconds) for the
+    searches -- overflow_count is the 16-bit count, or (o8, o16) for the
+    8-bit mode 7; with chunk_counts the per-chunk [nchunks, 2] (o8, o16)
+    array is appended.  views: a list of equal-length query views (searched
+    as one multi-view query) instead of `query`."""
+    nviews = 0
+    if views is not None:
+        nviews = len(views)
+        query = np.concatenate([np.asarray(v, np.uint8) for v in views])
     if query is None:
         query = np.zeros(0, np.uint8)
     if matrix is None:
@@ -206,7 +245,7 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
         db, off = pack_db(seqs or [])
     nseq = len(off) - 1
     hdr = b"SSAR" + struct.pack("<IIIQQiiII", mode, algo, threads, k, chunk, gap_open, gap_extend,
-                                repeat, 0)
+                                repeat, nviews)
     with tempfile.TemporaryDirectory() as td:
         req = os.path.join(td, "req.bin")
         rsp = os.path.join(td, "rsp.bin")
@@ -254,4 +293,10 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
     pos = 8 + 16 * cnt
     ovf, ns = struct.unpack_from("<QQ", data, pos)
     secs = struct.unpack_from("<d", data, pos + 16)[0]
+    o8, nch = struct.unpack_from("<QQ", data, pos + 24)
+    if mode == MODE_SEARCH8_AVX2:
+        ovf = (o8, ovf)
+    if chunk_counts:
+        per = np.frombuffer(data, dtype=np.uint64, count=2 * nch, offset=pos + 40).reshape(nch, 2).copy()
+        return hits, ovf, ns, secs, per
     return hits, ovf, ns, secs

@@ -25,6 +25,17 @@
  *        6 = COMPUTE_ALIGNMENT traceback (align.c align_sequences) of the
  *            query against every DB sequence: u64 region[4] (q begin, q end,
  *            d begin, d end), u64 cigar length, cigar bytes
+ *        7 = 8-bit AVX2 search: per chunk the reference's int8 kernel for
+ *            every query, its overflow chunk re-run by search_16_chunk
+ *            (the cascade of search_8.c:94-124, restated here because
+ *            search_8_chunk is static)
+ * Search modes (1, 2, 3, 7) answer: u64 count, (i64 score, u64 id) x count,
+ * u64 16-bit overflows, u64 non-empty sequences, f64 best seconds, u64
+ * 8-bit overflows, u64 nchunks, (u64 o8, u64 o16) per chunk (with chunk = 1:
+ * per-sequence overflow flags).
+ * The header's pad field is the number of query views (0 or 1: one); the
+ * query blob then holds that many views of qlen / views residues each
+ * (e.g. both strands of a nucleotide query, searcher.c:42-90).
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -45,6 +56,8 @@
 #include "algo/searcher.h"
 #include "algo/gap_costs.h"
 #include "algo/16/search_16.h"
+#include "algo/8/search_8.h"
+#include "algo/8/search_8_util.h"
 #include "algo/64/search_64.h"
 #include "algo/align.h"
 
@@ -62,7 +75,7 @@ static double now(void) {
 }
 
 typedef struct {
-    uint32_t mode, algo, threads; uint64_t k, chunk; int32_t gO, gE; uint32_t repeat;
+    uint32_t mode, algo, threads; uint64_t k, chunk; int32_t gO, gE; uint32_t repeat, views;
     int64_t mat[1024];
     uint64_t qlen; uint8_t* q;
     uint64_t nseq; uint64_t* off; uint8_t* db;
@@ -78,7 +91,8 @@ static size_t NCHUNKS;
 static size_t NEXT_CHUNK;
 static pthread_mutex_t MTX = PTHREAD_MUTEX_INITIALIZER;
 
-typedef struct { p_minheap heap; size_t ovf; } tres_t;
+typedef struct { p_minheap heap; size_t ovf, ovf8; } tres_t;
+static uint64_t* CH_OVF;          /* per chunk: (8-bit, 16-bit) overflow counts */
 
 static size_t claim(void) {
     pthread_mutex_lock(&MTX);
@@ -90,21 +104,44 @@ static size_t claim(void) {
 static void* worker(void* arg) {
     tres_t* res = (tres_t*)arg;
     res->heap = minheap_init(R.k);
-    res->ovf = 0;
+    res->ovf = res->ovf8 = 0;
     db_chunk_t chunk;
     p_s16info s16 = NULL;
+    p_s8info s8 = NULL;
     int64_t* he = NULL;
-    if (R.mode == 2 || R.mode == 3) s16 = search_16_init(SDP);
-    else he = search_64_alloc_hearray(SDP);
+    if (R.mode == 2 || R.mode == 3 || R.mode == 7) s16 = search_16_init(SDP);
+    if (R.mode == 7) s8 = search_8_init(SDP);
+    if (!s16) he = search_64_alloc_hearray(SDP);
     for (;;) {
         size_t c = claim();
         if (c >= NCHUNKS) break;
         chunk.seq = SEQS + CHUNK_BEGIN[c];
         chunk.fill_pointer = CHUNK_BEGIN[c + 1] - CHUNK_BEGIN[c];
         chunk.size = chunk.fill_pointer;
-        if (s16) res->ovf += search_16_chunk(s16, res->heap, &chunk, SDP);
-        else search_64_chunk(res->heap, &chunk, SDP, he);
+        uint64_t o8 = 0, o16 = 0;
+        if (s8) {
+            /* search_8.c:94-124 */
+            p_db_chunk ovf = adp_alloc_chunk(chunk.size * SDP->q_count + 1);
+            for (uint8_t q = 0; q < SDP->q_count; q++) {
+                if (R.algo == 0) search_8_avx2_sw(s8, &chunk, res->heap, ovf, q);
+                else search_8_avx2_nw(s8, &chunk, res->heap, ovf, q);
+            }
+            if (ovf->fill_pointer) {
+                o8 = ovf->fill_pointer;
+                o16 = search_16_chunk(s16, res->heap, ovf, SDP);
+            }
+            adp_free_chunk_no_sequences(ovf);
+        } else if (s16) {
+            o16 = search_16_chunk(s16, res->heap, &chunk, SDP);
+        } else {
+            search_64_chunk(res->heap, &chunk, SDP, he);
+        }
+        res->ovf8 += o8;
+        res->ovf += o16;
+        CH_OVF[2 * c] = o8;
+        CH_OVF[2 * c + 1] = o16;
     }
+    if (s8) search_8_exit(s8);
     if (s16) search_16_exit(s16);
     if (he) free(he);
     return NULL;
@@ -114,10 +151,13 @@ static void run_search(FILE* out) {
     /* query buffer (AMINOACID-style single query; symbol type does not
      * matter below the searcher for pre-mapped codes) */
     SDP = (p_search_data)calloc(1, sizeof(search_data_t));
-    SDP->q_count = 1;
-    SDP->maxqlen = R.qlen;
-    SDP->queries[0].seq.seq = (char*)R.q;
-    SDP->queries[0].seq.len = R.qlen;
+    const uint32_t nq = R.views > 1 ? R.views : 1;
+    SDP->q_count = (uint8_t)nq;
+    SDP->maxqlen = R.qlen / nq;
+    for (uint32_t v = 0; v < nq; v++) {
+        SDP->queries[v].seq.seq = (char*)R.q + v * (R.qlen / nq);
+        SDP->queries[v].seq.len = R.qlen / nq;
+    }
 
     score_matrix_64 = (int64_t*)aligned_alloc(64, sizeof(int64_t) * 1024);
     score_matrix_16 = (int16_t*)aligned_alloc(64, sizeof(int16_t) * 1024);
@@ -134,6 +174,7 @@ static void run_search(FILE* out) {
     if (R.mode == 3) set_max_compute_capability(COMPUTE_ON_SSE2);
     search_64_init_algo(R.algo);
     search_16_init_algo(R.algo);
+    search_8_init_algo(R.algo);
 
     /* non-empty sequences in ID order; chunks are ID ranges of R.chunk IDs
      * with empty sequences skipped (db_adapter.c:212-239) */
@@ -152,13 +193,14 @@ static void run_search(FILE* out) {
         SEQS[NSEQS++] = s;
     }
     CHUNK_BEGIN[NCHUNKS] = NSEQS;
+    CH_OVF = (uint64_t*)calloc(2 * NCHUNKS + 2, sizeof(uint64_t));
 
     int T = R.threads ? (int)R.threads : 1;
     tres_t* res = (tres_t*)calloc(T, sizeof(tres_t));
     pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
     double best = 1e30;
     p_minheap merged = NULL;
-    size_t ovf = 0;
+    size_t ovf = 0, ovf8 = 0;
     for (uint32_t rep = 0; rep < (R.repeat ? R.repeat : 1); rep++) {
         if (merged) minheap_exit(merged);
         for (int t = 0; t < T; t++) if (res[t].heap) { minheap_exit(res[t].heap); res[t].heap = NULL; }
@@ -168,10 +210,11 @@ static void run_search(FILE* out) {
         for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
         /* merge in thread order (manager.c:141-145) */
         merged = minheap_init(R.k);
-        ovf = 0;
+        ovf = ovf8 = 0;
         for (int t = 0; t < T; t++) {
             for (size_t j = 0; j < res[t].heap->count; j++) minheap_add(merged, &res[t].heap->array[j]);
             ovf += res[t].ovf;
+            ovf8 += res[t].ovf8;
         }
         minheap_sort(merged);
         double dt = now() - t0;
@@ -190,6 +233,10 @@ static void run_search(FILE* out) {
     uint64_t ns = NSEQS;
     fwrite(&ns, 8, 1, out);
     fwrite(&best, 8, 1, out);
+    uint64_t o8 = ovf8, nch = NCHUNKS;
+    fwrite(&o8, 8, 1, out);
+    fwrite(&nch, 8, 1, out);
+    fwrite(CH_OVF, 8, 2 * NCHUNKS, out);
 }
 
 static void run_scores(FILE* out) {
@@ -265,7 +312,7 @@ int main(int argc, char** argv) {
     rd(&R.mode, 4, f); rd(&R.algo, 4, f); rd(&R.threads, 4, f);
     rd(&R.k, 8, f); rd(&R.chunk, 8, f);
     rd(&R.gO, 4, f); rd(&R.gE, 4, f); rd(&R.repeat, 4, f);
-    uint32_t pad; rd(&pad, 4, f);
+    rd(&R.views, 4, f);
     rd(R.mat, 8 * 1024, f);
     rd(&R.qlen, 8, f);
     R.q = (uint8_t*)malloc(R.qlen + 1);

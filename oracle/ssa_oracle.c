@@ -210,6 +210,216 @@ int64_t oracle_full_nw(const uint8_t* d, size_t dlen, const uint8_t* q, size_t q
     return hearray[2 * qlen - 2];
 }
 
+/* ------------------------------------------------- 8/16-bit overflow flags */
+/* Whether the reference's w-bit SIMD NW kernel (w = 8 or 16) sends one
+ * (query, DB sequence) pair to the next width, i.e. counts it in
+ * overflow_{w}_bit_count.  Replays, for one channel, the saturated int_w
+ * recurrence of search_simd_nw.c:180-503:
+ *   - the DB sequence runs in blocks of CDEPTH = 4 columns, the last one
+ *     padded with code 0 (move_db_sequence_window_*, search_16_util.h:66-80);
+ *   - first block: top diagonals H0..H3 = 0, Q+R, Q+2R, Q+3R and top F
+ *     F0..F3 = Q+R .. Q+4R, computed in int and truncated to int_w
+ *     (:445-453); later blocks continue both with saturating +R (:494-502);
+ *     the F entering row 0 is F_k + QR (:211-214);
+ *   - left boundary (new sequence): H(i,-1) = QR + i*R and the incoming E
+ *     = H(i,-1) + QR, both saturating chains (:233-240);
+ *   - ALIGNCORE (:180-191) with saturating adds; h_min / h_max start at 0
+ *     (:202-203) and collect every H of every processed cell;
+ *   - overflow iff h_min < trunc(I_MIN - Q - R - 1) or h_max == I_MAX
+ *     (:372-373, 483-485), or the score H(qlen-1, dlen-1) is not strictly
+ *     inside (I_MIN, I_MAX) (:426).
+ * V = (int_w) M[d][q] (the 8/16-bit score tables truncate, matrices.c:375-376).
+ * work: 2 * qlen int64.  qlen and dlen must be > 0. */
+static int64_t trunc_w(int64_t v, int w) { return w == 8 ? (int64_t)(int8_t)v : (int64_t)(int16_t)v; }
+
+static int64_t sat_w(int64_t v, int w) {
+    const int64_t lo = -((int64_t)1 << (w - 1)), hi = ((int64_t)1 << (w - 1)) - 1;
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+int oracle_nw_overflow(int w, const uint8_t* d, size_t dlen, const uint8_t* q, size_t qlen,
+                       const int64_t* m, int gapO, int gapE, int64_t* work) {
+    const int64_t IMIN = -((int64_t)1 << (w - 1)), IMAX = ((int64_t)1 << (w - 1)) - 1;
+    const int64_t QR = trunc_w(gapO + gapE, w), R = trunc_w(gapE, w);
+    const int64_t T = trunc_w(IMIN - gapO - gapE - 1, w);
+    int64_t* hep = work;
+    int64_t mge = QR;
+    for (size_t i = 0; i < qlen; i++) {
+        hep[2 * i] = sat_w(mge, w);
+        hep[2 * i + 1] = sat_w(sat_w(mge, w) + QR, w);
+        mge = sat_w(mge + R, w);
+    }
+    int64_t Ht[4], Ft[4];
+    for (int k = 0; k < 4; k++) {
+        Ht[k] = k == 0 ? 0 : trunc_w(gapO + (int64_t)k * gapE, w);
+        Ft[k] = trunc_w(gapO + (int64_t)(k + 1) * gapE, w);
+    }
+    int64_t hmin = 0, hmax = 0, score = 0;
+    const size_t nblocks = (dlen + 3) / 4;
+    for (size_t b = 0; b < nblocks; b++) {
+        int64_t h[4], f[4], V[4];
+        const int64_t* row[4];
+        for (int k = 0; k < 4; k++) {
+            const size_t j = 4 * b + k;
+            row[k] = m + ((size_t)(j < dlen ? d[j] : 0) << 5);
+            h[k] = Ht[k];
+            f[k] = sat_w(Ft[k] + QR, w);
+        }
+        for (size_t i = 0; i < qlen; i++) {
+            const int64_t h4 = hep[2 * i];
+            int64_t E = hep[2 * i + 1], N[4];
+            for (int k = 0; k < 4; k++) V[k] = trunc_w(row[k][q[i]], w);
+            for (int k = 0; k < 4; k++) {
+                int64_t H = sat_w(h[k] + V[k], w);
+                if (f[k] > H) H = f[k];
+                if (E > H) H = E;
+                if (H < hmin) hmin = H;
+                if (H > hmax) hmax = H;
+                N[k] = H;
+                H = sat_w(H + QR, w);
+                f[k] = sat_w(f[k] + R, w);
+                if (H > f[k]) f[k] = H;
+                E = sat_w(E + R, w);
+                if (H > E) E = H;
+            }
+            hep[2 * i] = N[3];
+            hep[2 * i + 1] = E;
+            if (i + 1 == qlen && b + 1 == nblocks) score = N[(dlen + 3) % 4];
+            h[0] = h4; h[1] = N[0]; h[2] = N[1]; h[3] = N[2];
+        }
+        const int64_t F3 = Ft[3], H3 = Ht[3];
+        Ft[0] = sat_w(F3 + R, w); Ft[1] = sat_w(Ft[0] + R, w); Ft[2] = sat_w(Ft[1] + R, w); Ft[3] = sat_w(Ft[2] + R, w);
+        Ht[0] = sat_w(H3 + R, w); Ht[1] = sat_w(Ht[0] + R, w); Ht[2] = sat_w(Ht[1] + R, w); Ht[3] = sat_w(Ht[2] + R, w);
+    }
+    return hmin < T || hmax == IMAX || score <= IMIN || score >= IMAX;
+}
+
+/* Same for the w-bit SIMD SW kernel (search_simd_sw.c:172-441): values
+ * biased by -2^(w-1) so the local floor is the saturation floor; every
+ * block starts its top row and F at I_MIN (:188-189); a new sequence's left
+ * column H and E are I_MIN (:205-212); S = max of every H incl. the padding
+ * columns; overflow iff S reaches I_MAX (:372-378, 422-423).  With Q, R <= 0,
+ * Q + R and the matrix inside int_w this is "score >= 2^w - 1"; large or
+ * positive penalties make the truncated Q+R behave differently. */
+int oracle_sw_overflow(int w, const uint8_t* d, size_t dlen, const uint8_t* q, size_t qlen,
+                       const int64_t* m, int gapO, int gapE, int64_t* work) {
+    const int64_t IMIN = -((int64_t)1 << (w - 1)), IMAX = ((int64_t)1 << (w - 1)) - 1;
+    const int64_t QR = trunc_w(gapO + gapE, w), R = trunc_w(gapE, w);
+    int64_t* hep = work;
+    for (size_t i = 0; i < 2 * qlen; i++) hep[i] = IMIN;
+    int64_t S = IMIN;
+    const size_t nblocks = (dlen + 3) / 4;
+    for (size_t b = 0; b < nblocks; b++) {
+        int64_t h[4], f[4];
+        const int64_t* row[4];
+        for (int k = 0; k < 4; k++) {
+            const size_t j = 4 * b + k;
+            row[k] = m + ((size_t)(j < dlen ? d[j] : 0) << 5);
+            h[k] = IMIN;
+            f[k] = IMIN;
+        }
+        for (size_t i = 0; i < qlen; i++) {
+            const int64_t h4 = hep[2 * i];
+            int64_t E = hep[2 * i + 1], N[4];
+            for (int k = 0; k < 4; k++) {
+                int64_t H = sat_w(h[k] + trunc_w(row[k][q[i]], w), w);
+                if (f[k] > H) H = f[k];
+                if (E > H) H = E;
+                if (H > S) S = H;
+                N[k] = H;
+                H = sat_w(H + QR, w);
+                f[k] = sat_w(f[k] + R, w);
+                if (H > f[k]) f[k] = H;
+                E = sat_w(E + R, w);
+                if (H > E) E = H;
+            }
+            hep[2 * i] = N[3];
+            hep[2 * i + 1] = E;
+            h[0] = h4; h[1] = N[0]; h[2] = N[1]; h[3] = N[2];
+        }
+        if (S == IMAX) return 1;
+    }
+    return 0;
+}
+
+/* The reference's overflow counters of one search (m_run's INFO line,
+ * manager.c:157-160), from per-(view, sequence) scores or flags.  For
+ * every DB sequence e with views v: a8(e) = #v overflowing at 8 bits,
+ * a16(e) = #v overflowing at 16 bits.  SW overflows at w bits iff the
+ * score is >= 2^w - 1 under ordinary penalties (oracle_sw_overflow); NW per
+ * oracle_nw_overflow.
+ *   width 16: o16 = sum a16(e)                        (search_16.c:92-114)
+ *   width 8:  o8 = sum a8(e), o16 = sum a8(e) * a16(e) -- the 8-bit overflow
+ *             chunk holds e once per overflowing view and search_16_chunk
+ *             re-runs every copy for every view (search_8.c:94-124).
+ * flags: [views][nseq] bytes, bit 0 = 8-bit, bit 1 = 16-bit overflow. */
+void oracle_overflow_counts(int width, const uint8_t* flags, size_t views, size_t nseq, uint64_t out[2]) {
+    uint64_t o8 = 0, o16 = 0;
+    for (size_t e = 0; e < nseq; e++) {
+        uint64_t a8 = 0, a16 = 0;
+        for (size_t v = 0; v < views; v++) {
+            a8 += flags[v * nseq + e] & 1;
+            a16 += (flags[v * nseq + e] >> 1) & 1;
+        }
+        if (width == 8) {
+            o8 += a8;
+            o16 += a8 * a16;
+        } else if (width == 16) {
+            o16 += a16;
+        }
+    }
+    out[0] = o8;
+    out[1] = o16;
+}
+
+/* Per-sequence overflow flags of every DB sequence (bit 0: 8-bit, bit 1:
+ * 16-bit), multithreaded.  algo 0 = SW, 1 = NW (saturated replays). */
+typedef struct {
+    int algo; const uint8_t* db; const uint64_t* off; const uint8_t* q; size_t qlen;
+    const int64_t* m; int gO, gE; uint8_t* out; size_t begin, end;
+} flag_job_t;
+
+static void* run_flag_job(void* p) {
+    flag_job_t* J = (flag_job_t*)p;
+    int64_t* he = (int64_t*)malloc(sizeof(int64_t) * 2 * (J->qlen + 1));
+    for (size_t k = J->begin; k < J->end; k++) {
+        const uint8_t* d = J->db + J->off[k];
+        size_t dl = (size_t)(J->off[k + 1] - J->off[k]);
+        uint8_t f = 0;
+        if (dl > 0 && J->qlen > 0) {
+            if (J->algo == 0) {
+                f = (uint8_t)(oracle_sw_overflow(8, d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he) |
+                              (oracle_sw_overflow(16, d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he) << 1));
+            } else {
+                f = (uint8_t)(oracle_nw_overflow(8, d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he) |
+                              (oracle_nw_overflow(16, d, dl, J->q, J->qlen, J->m, J->gO, J->gE, he) << 1));
+            }
+        }
+        J->out[k] = f;
+    }
+    free(he);
+    return NULL;
+}
+
+void oracle_overflow_flags(int algo, const uint8_t* db, const uint64_t* offsets, size_t nseq,
+                           const uint8_t* q, size_t qlen, const int64_t* m, int gapO, int gapE,
+                           uint8_t* out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > nseq) nthreads = nseq ? (int)nseq : 1;
+    pthread_t th[256];
+    flag_job_t jobs[256];
+    size_t per = (nseq + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        flag_job_t J = {algo, db, offsets, q, qlen, m, gapO, gapE, out, t * per, (t + 1) * per};
+        if (J.begin > nseq) J.begin = nseq;
+        if (J.end > nseq) J.end = nseq;
+        jobs[t] = J;
+        pthread_create(&th[t], NULL, run_flag_job, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
 /* Scores every DB sequence (concatenated codes, offsets[k]..offsets[k+1])
  * against one query.  algo: 0 = SW, 1 = NW.  Multithreaded, order-free. */
 typedef struct {

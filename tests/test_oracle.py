@@ -140,3 +140,47 @@ def test_heap_tie_semantics_small():
     assert po.topk(np.array([5, 5, 5]), np.array([0, 1, 2]), 2) == [(5, 1), (5, 0)]
     # order: score desc, then id desc
     assert po.topk(np.array([1, 3, 3, 2]), np.array([0, 1, 2, 3]), 3) == [(3, 2), (3, 1), (2, 3)]
+
+
+# ------------------------------------------------------------ overflow counters
+OVF = np.load(os.path.join(GOLDEN, "overflow.npz"))
+OVF_CASES = json.loads(str(OVF["meta"]))
+
+
+def _ovf_matrix(c):
+    if c["matrix"] == "const":
+        return po.matrix_constant(c["match"], c["mismatch"])
+    return TABLES["matrices"][NAMES.index(c["matrix"])].copy()
+
+
+@pytest.mark.parametrize("case", OVF_CASES, ids=[f"c{c['id']}" for c in OVF_CASES])
+def test_overflow_flags_match_reference(case):
+    """Per-sequence 8/16-bit overflow flags of the reference's SIMD kernels
+    (harness with chunk size 1, tools/gen_golden.py gen_overflow) equal the
+    oracle's saturated replays -- ordinary penalties and ones whose int8 sum
+    wraps or is positive (search_simd_sw.c / search_simd_nw.c)."""
+    t = case["id"]
+    q, db, off = OVF[f"c{t}_q"], OVF[f"c{t}_db"], OVF[f"c{t}_off"]
+    got = po.overflow_flags(case["algo"], q, db, off, _ovf_matrix(case), case["gap_open"], case["gap_extend"])
+    exp = OVF[f"c{t}_flags"]
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+
+
+@pytest.mark.parametrize("case", KATS, ids=[c["name"] for c in KATS])
+def test_kat_overflow_counters(case):
+    """m_run's counters (manager.c:157-160) for every KAT at widths 8 and 16,
+    from the oracle's flags, equal the reference's (incl. the KATs written in
+    its tests: overflow_127 1/1, sw_overflow_534 1/0, test.fas NW int8 4/0)."""
+    qc, seqs, M = kat_inputs(case)
+    db, off = po.pack_db(seqs)
+    keep = np.diff(off) > 0
+    for algo, an in ((0, "sw"), (1, "nw")):
+        f = po.overflow_flags(algo, qc, db, off, M, case["gap_open"], case["gap_extend"])[keep]
+        assert po.overflow_counts(8, f) == tuple(case[an + "_8_overflow"]), an
+        assert po.overflow_counts(16, f)[1] == case[an + "_16_overflow"], an
+    fixed = {"overflow_127": ((1, 1), (1, 1)), "sw_overflow_534": ((1, 0), None),
+             "search64_test_fas": (None, (4, 0))}
+    if case["name"] in fixed:
+        for algo, exp in enumerate(fixed[case["name"]]):
+            if exp is not None:
+                assert tuple(case[("sw", "nw")[algo] + "_8_overflow"]) == exp

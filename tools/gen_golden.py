@@ -23,6 +23,17 @@ outputs as data:
                                parameters by libssa_amd.synthetic) with the
                                reference's full int64 score vector (full_sw /
                                full_nw) and its 64-bit top-k for several k
+  tests/golden/overflow.npz    the reference's own 8- and 16-bit overflow
+                               flags of every sequence of seeded random cases
+                               (chunk size 1: one count per sequence), SW and
+                               NW, ordinary and pathological gap penalties
+  tests/golden/fullsize.json   BASELINE.json's configurations at full (C2, C3:
+                               1 M sequences) or share (C4: the first 1.25 M of
+                               the 10 M DB, C5: the first 1 M of the 50 M
+                               reads) size, plus the 25- and 28-symbol
+                               alphabets: SHA-256 of the reference's full
+                               score vector, its histogram, the top-k, and
+                               the reference's overflow counters
 """
 import hashlib
 import json
@@ -40,6 +51,15 @@ G = os.path.join(ROOT, "tests", "golden")
 D = os.path.join(G, "data")
 NAMES = ["blosum45", "blosum50", "blosum62", "blosum80", "blosum90", "pam30", "pam70", "pam250"]
 
+# query of tests/algo/8/test_8_simd_avx2_sw.c:106-113 (one C string literal)
+OVF534_QUERY = ("MVQRWLYSTNAKDIAVLYFMLAIFSGMAGTAMSLIIRLELAAPGSQYLHGNSQLFNVLVVGHAVLMIFFLVMPALIGGFG"
+                "NYLLPLMIGATDTAFPRINNIAFWVLPMGLVCLVTSTLVESGAGTGWTVYPPLSSIQAHSGPSVDLAIFALHLTSISSLL"
+                "GAINFIVTTLNMRTNGMTMHKLPLFVWSIFITAFLLLLSLPVLSAGITMLLLDRNFNTSFFEVSGGGDPILYEHLFWFFG"
+                "HPEVYILIIPGFGIISHVVSTYSKKPVFGEISMVYAMASIGLLGFLVWSHHMYIVGLDADTRAYFTSATMIIAIPTGIKI"
+                "FSWLATIHGGSIRLATPMLYAIAFLFLFTMGGLTGVALANASLDVAFHDTYYVVGHFHYVLSMGAIFSLFAGYYYWSPQI"
+                "LGLNYNEKLAQIQFWLIFIGANVIFFPMHFLGINGMPRRIPDYPDAFAGWNYVASIGSFIATLSLFLFIYILYDQLVNGL"
+                "NNKVNNKSVIYNKAPDFVESNTIFNLNTVKSSSIEFLLTSPPAVHSFNTPAVQS")
+
 # (name, db file, nucleotide, query (file: or str:), scoring, gapO, gapE, k, chunk)
 KATS = [
     ("libssa_const5_4", "AF091148.fas", True, "file:one_seq.fas", ("const", 5, -4), -4, -2, 5, 1000),
@@ -56,6 +76,8 @@ KATS = [
      ("builtin", "blosum62"), -1, -1, 1, 1),
     ("overflow_127", "NP_009305.1.fas", False, "file:NP_009305.1.fas", ("const", 127, -1), -1, -1, 1, 1),
     ("tmp_fas_8bit", "tmp.fas", True, "str:ATGCAAA", ("const", 1, -1), -1, -1, 1, 1),
+    # tests/algo/8/test_8_simd_avx2_sw.c:104-124: 534, one 8-bit overflow
+    ("sw_overflow_534", "NP_009305.1.fas", False, "str:" + OVF534_QUERY, ("const", 1, -1), -1, -1, 1, 1),
     ("config1_Q3ZAI3", "AF091148.fas", False, "file:Q3ZAI3.fasta", ("builtin", "blosum62"), -11, -1, 10, 1000),
     ("config1_Q3ZAI3_k300", "AF091148.fas", False, "file:Q3ZAI3.fasta", ("builtin", "blosum62"), -11, -1, 300, 1000),
     ("nt_file_matrix", "AF091148.fas", True, "file:one_seq.fas", ("file", "nuc_scoring_matrix.txt"), -3, -1, 20, 1000),
@@ -94,9 +116,11 @@ def main():
         for algo, an in ((0, "sw"), (1, "nw")):
             hits64, _, ns, _ = po.ref_run(po.MODE_SEARCH64, algo, qc, seqs, M, go, ge, k=k, chunk=chunk)
             hits16, ovf16, _, _ = po.ref_run(po.MODE_SEARCH16_AVX2, algo, qc, seqs, M, go, ge, k=k, chunk=chunk)
+            _, ovf8, _, _ = po.ref_run(po.MODE_SEARCH8_AVX2, algo, qc, seqs, M, go, ge, k=k, chunk=chunk)
             case[an + "_64"] = hits64
             case[an + "_16_avx2"] = hits16
             case[an + "_16_overflow"] = int(ovf16)
+            case[an + "_8_overflow"] = [int(x) for x in ovf8]
             case["nseq_nonempty"] = int(ns)
         kats.append(case)
         print(name, "sw", case["sw_64"][:3], "nw", case["nw_64"][:3])
@@ -214,8 +238,128 @@ def gen_align():
     print("align ok", len(out), "pairs")
 
 
+def gen_overflow():
+    """Per-sequence 8/16-bit overflow flags from the reference (the
+    harness with chunk size 1 reports one overflow count per sequence)."""
+    rng = np.random.default_rng(31)
+    mats = po.ref_run(po.MODE_TABLES)[0]
+    arrays, cases = {}, []
+    for t in range(40):
+        algo = t % 2
+        mname = ["blosum62", "blosum50", "pam30", "const"][(t // 2) % 4]
+        if mname == "const":
+            match, mismatch = int(rng.integers(1, 128)), int(rng.integers(-20, 0))
+            M = po.matrix_constant(match, mismatch)
+        else:
+            match = mismatch = 0
+            M = mats[NAMES.index(mname)].copy()
+        # ordinary penalties mostly; a few whose int8 sum wraps or is positive
+        go = int(rng.choice([-1, -3, -5, -11, -11, -40, -100, 0, 5]))
+        ge = int(rng.choice([-1, -1, -2, -4, -10, -50, 0, 3]))
+        qlen = int(rng.choice([1, 2, 5, 17, 60, 130, 300, 700]))
+        q = rng.choice(syn.AA_CODES, qlen).astype(np.uint8)
+        lens = rng.integers(1, 400, 300)
+        seqs = [rng.choice(syn.AA_CODES, int(n)).astype(np.uint8) for n in lens]
+        for i in range(0, 300, 7):
+            seqs[i] = q[: max(1, qlen - int(rng.integers(0, 5)))].copy()
+        _, _, _, _, per8 = po.ref_run(po.MODE_SEARCH8_AVX2, algo, q, seqs, M, go, ge, k=5, chunk=1, threads=8,
+                                      chunk_counts=True)
+        _, _, _, _, per16 = po.ref_run(po.MODE_SEARCH16_AVX2, algo, q, seqs, M, go, ge, k=5, chunk=1, threads=8,
+                                       chunk_counts=True)
+        db, off = po.pack_db(seqs)
+        arrays[f"c{t}_q"] = q
+        arrays[f"c{t}_db"] = db
+        arrays[f"c{t}_off"] = off
+        arrays[f"c{t}_flags"] = (per8[:, 0].astype(np.uint8) | (per16[:, 1].astype(np.uint8) << 1))
+        cases.append({"id": t, "algo": algo, "matrix": mname, "match": match, "mismatch": mismatch,
+                      "gap_open": go, "gap_extend": ge})
+        print("overflow case", t, algo, mname, go, ge, qlen, int(per8[:, 0].sum()), int(per16[:, 1].sum()))
+    np.savez_compressed(os.path.join(G, "overflow.npz"), meta=np.array(json.dumps(cases)), **arrays)
+
+
+# BASELINE.json configurations for the full-size fixtures (bench.py builds the
+# same DBs from the same parameters): the block-seeded generators of
+# libssa_amd.synthetic, so a share is the first IDs of the whole DB
+FULLSIZE = {
+    "c2": dict(kind="protein", n=1_000_000, i1=1_000_000, seed=42, qlen=400, qseed=7, matrix="blosum62",
+               gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="bg20"),
+    "c3": dict(kind="protein", n=1_000_000, i1=1_000_000, seed=42, qlen=1000, qseed=7, matrix="blosum50",
+               gap_open=-10, gap_extend=-2, algo="nw", width=16, alphabet="bg20"),
+    "c4": dict(kind="protein", n=10_000_000, i1=1_250_000, seed=42, qlen=400, qseed=7, matrix="blosum62",
+               gap_open=-11, gap_extend=-1, algo="sw", width=8, alphabet="bg20"),
+    "c5": dict(kind="dna", n=50_000_000, i1=1_000_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
+               gap_open=-4, gap_extend=-2, algo="sw", width=16),
+    "sp25": dict(kind="protein", n=500_000, i1=500_000, seed=44, qlen=400, qseed=7, matrix="blosum62",
+                 gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="sprot25"),
+    "u28": dict(kind="protein", n=200_000, i1=200_000, seed=45, qlen=400, qseed=7, matrix="blosum62",
+                gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="uniform28", lengths="uniform",
+                lo=16, hi=1000),
+    "u28nw": dict(kind="protein", n=200_000, i1=200_000, seed=45, qlen=400, qseed=7, matrix="blosum62",
+                  gap_open=-11, gap_extend=-1, algo="nw", width=16, alphabet="uniform28", lengths="uniform",
+                  lo=16, hi=1000),
+}
+
+
+def fullsize_db(c):
+    """(query codes, DB codes, offsets) of a FULLSIZE entry."""
+    if c["kind"] == "dna":
+        q = syn.dna_query(c["qlen"], c["qseed"])
+        codes, off = syn.dna_reads_range(c["n"], c["seed"], 0, c["i1"], 150, query=q)
+        return q, codes, off
+    q = syn.protein_query(c["qlen"], c["qseed"])
+    codes, off = syn.protein_db_range(c["n"], c["seed"], 0, c["i1"], query=q, alphabet=c.get("alphabet", "bg20"),
+                                      lengths=c.get("lengths", "gamma"), lo=c.get("lo", 16), hi=c.get("hi", 4096))
+    return q, codes, off
+
+
+def gen_fullsize(names=None):
+    mats = po.ref_run(po.MODE_TABLES)[0]
+    path = os.path.join(G, "fullsize.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for name, c in FULLSIZE.items():
+        if names and name not in names:
+            continue
+        q, codes, off = fullsize_db(c)
+        if c["matrix"].startswith("const"):
+            a, b = c["matrix"][5:].split("_")
+            M = po.matrix_constant(int(a), int(b))
+        else:
+            M = mats[NAMES.index(c["matrix"])].copy()
+        n = len(off) - 1
+        algo = 0 if c["algo"] == "sw" else 1
+        mode = po.MODE_SEARCH8_AVX2 if c["width"] == 8 else po.MODE_SEARCH16_AVX2
+        import time
+        t0 = time.time()
+        # k = n: every (score, id) stays in the reference's heap
+        hits, ovf, ns, secs = po.ref_run(mode, algo, q, None, M, c["gap_open"], c["gap_extend"], k=n, threads=8,
+                                         db_off=(codes, off))
+        assert ns == n == len(hits)
+        arr = np.array(hits, dtype=np.int64)
+        order = np.argsort(arr[:, 1], kind="stable")
+        ids, sc = arr[order, 1], arr[order, 0]
+        assert (ids == np.arange(n)).all()
+        vals, counts = np.unique(sc, return_counts=True)
+        rec = dict(c)
+        rec.update({"nonempty": int(ns), "residues": int(off[-1]),
+                    "sha256": hashlib.sha256(sc.astype("<i8").tobytes()).hexdigest(),
+                    "hist_values": vals.tolist(), "hist_counts": counts.tolist(),
+                    "overflow": list(ovf) if c["width"] == 8 else [0, int(ovf)],
+                    "ref_seconds": round(secs, 2)})
+        # the 64-bit single-thread result = the reference heap fed in ID order
+        # (SURVEY.md §8c; the oracle heap is pinned by tests/test_oracle.py)
+        for k in (1, 10, 64):
+            rec[f"top{k}"] = po.topk(sc, ids.astype(np.uint64), k)
+        out[name] = rec
+        print(name, "ok", round(time.time() - t0, 1), "s", rec["top10"][:3], rec["overflow"])
+        json.dump(out, open(path, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "translate":
+    if len(sys.argv) > 1 and sys.argv[1] == "overflow":
+        gen_overflow()
+    elif len(sys.argv) > 1 and sys.argv[1] == "fullsize":
+        gen_fullsize(sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "translate":
         gen_translate()
     elif len(sys.argv) > 1 and sys.argv[1] == "align":
         gen_align()
@@ -223,3 +367,5 @@ if __name__ == "__main__":
         main()
         gen_translate()
         gen_align()
+        gen_overflow()
+        gen_fullsize()
