@@ -80,38 +80,6 @@ void replay(const SearchScores& sc, const EntryMeta& meta, const std::vector<Que
     }
 }
 
-void overflow_counters(const SearchScores& sc, int algo, int bw, uint64_t& o8, uint64_t& o16) {
-    o8 = o16 = 0;
-    if (bw == BIT_WIDTH_64) return;
-    if (sc.sparse) {
-        // device counts over the int32 scores + the exactly re-scored entries
-        o8 = bw == BIT_WIDTH_8 ? sc.dev_o8 : 0;
-        o16 = sc.dev_o16;
-        for (const auto& w : sc.wide) {
-            const int64_t s = w.second;
-            if (algo == kAlgoSW) {
-                if (bw == BIT_WIDTH_8 && s >= 255) o8++;
-                if (s >= 65535) o16++;
-            } else {
-                if (bw == BIT_WIDTH_8 && (s <= -128 || s >= 127)) o8++;
-                if (s <= -32768 || s >= 32767) o16++;
-            }
-        }
-        return;
-    }
-    for (size_t v = 0; v < sc.views; v++)
-        for (size_t e = 0; e < sc.entries; e++) {
-            const int64_t s = sc.get(v, e);
-            if (algo == kAlgoSW) {
-                if (bw == BIT_WIDTH_8 && s >= 255) o8++;
-                if (s >= 65535) o16++;
-            } else {
-                if (bw == BIT_WIDTH_8 && (s <= -128 || s >= 127)) o8++;
-                if (s <= -32768 || s >= 32767) o16++;
-            }
-        }
-}
-
 struct SearchResult {
     std::vector<QueryView> views;
     std::vector<Hit> hits;      // sorted top-k, or the insertion log
@@ -173,13 +141,12 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     }
     if (!want_log) R.hits = heap.sorted();
     const double t2 = now_ms();
+    // the reference's overflow counters, counted on the device
+    // (counters.hip): what its 8/16-bit kernels would have re-run
     uint64_t o8 = 0, o16 = 0;
     for (const SearchScores& x : sc) {
-        uint64_t a8 = 0, a16 = 0;
-        if (bw == BIT_WIDTH_8 || cfg().output_mode >= OUTPUT_INFO) overflow_counters(x, algo, bw, a8, a16);
-        else if (bw == BIT_WIDTH_16 && algo == kAlgoSW) a16 = x.wide.size();
-        o8 += a8;
-        o16 += a16;
+        o8 += x.dev_o8;
+        o16 += x.dev_o16;
     }
     publish_stats(sc, plan);
     ssa_amd_stats_t& S = stats();

@@ -45,6 +45,10 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch);
+    dfree(d_flags); dfree(d_flist); dfree(d_cnt);
+    if (h_cnt) (void)hipHostFree(h_cnt);
+    d_flags = nullptr; d_flist = nullptr; d_cnt = nullptr; h_cnt = nullptr;
+    flags_cap = 0;
     d_lscratch = nullptr;
     lscratch_cap = 0;
     d_upblk = nullptr;
@@ -76,7 +80,9 @@ void DeviceDB::release() {
     lane_out.clear();
 }
 
-constexpr size_t kOvfCap = 1 << 20;      // overflow list capacity per view
+constexpr size_t kOvfPinned = 4096;      // overflow entries the pinned mirrors hold (more: pageable copies)
+// per-search device upload block: [compact matrix 8 KiB][code-0 row 256 B][top boundary][query]
+constexpr size_t kUpHeader = 8192 + 256;
 
 // ------------------------------------------------------------ entry codes
 // Mapped residues of one entry, as db_adapter.c:47-110 builds them: NT codes
@@ -347,13 +353,18 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     }
     dalloc((void**)&D.d_scores, std::max<size_t>(E, 1) * 4, "scores");
     D.scores_cap = std::max<size_t>(E, 1);
-    dalloc((void**)&D.d_ovf, (kOvfCap + 1) * 4, "overflow list");
-    dalloc((void**)&D.d_wide, kOvfCap * 8, "wide scores");
-    D.upblk_cap = 8192 + 16384 + 4096;
+    // one view slice of the overflow list (grown per search for pipelined views)
+    dalloc((void**)&D.d_ovf, (H.lane_len.size() + 1) * 4, "overflow list");
+    dalloc((void**)&D.d_wide, std::max<size_t>(H.lane_len.size(), 1) * 8, "wide scores");
+    D.ovf_slices = 1;
+    dalloc((void**)&D.d_flist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
+    dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe, "overflow counters");
+    check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe, hipHostMallocDefault), "pinned");
+    D.upblk_cap = kUpHeader + 16384 + 4096;
     dalloc((void**)&D.d_upblk, D.upblk_cap, "per-search uploads");
     D.d_matrix = (int64_t*)D.d_upblk;
-    check(hipHostMalloc((void**)&D.h_ovf, (kOvfCap + 1) * 4, hipHostMallocDefault), "pinned");
-    check(hipHostMalloc((void**)&D.h_wide, kOvfCap * 8, hipHostMallocDefault), "pinned");
+    check(hipHostMalloc((void**)&D.h_ovf, (kOvfPinned + 1) * 4, hipHostMallocDefault), "pinned");
+    check(hipHostMalloc((void**)&D.h_wide, kOvfPinned * 8, hipHostMallocDefault), "pinned");
     check(hipMemcpy(D.d_groups, H.groups.data(), H.groups.size() * sizeof(GroupDesc), hipMemcpyHostToDevice), "H2D");
     check(hipMemcpy(D.d_res, H.res.data(), H.res.size(), hipMemcpyHostToDevice), "H2D residues");
     check(hipMemcpy(D.d_lane_len, H.lane_len.data(), H.lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
@@ -654,6 +665,8 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
     const Config& C = cfg();
     const uint32_t need = (uint32_t)((beyond + 63) / 64);
     if (C.long_groups == 0 || D.ngroups == 0 || D.alpha > 32) return need ? UINT32_MAX : 0;
+    // long_kernel's SW clamps E and F at 0: exact only for R <= 0
+    if (Q > 0 || R > 0) return need ? UINT32_MAX : 0;
     const int64_t amp = std::max(std::abs(minM), std::abs(maxM)) + std::abs((int64_t)Q) + std::abs((int64_t)R);
     if ((int64_t)(m + D.len_sorted.back() + 2) * amp >= (1ll << 30)) return need ? UINT32_MAX : 0;
     uint32_t g = 0;
@@ -699,6 +712,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.cells = 0;
     out.cand.clear();
     out.dev_o8 = out.dev_o16 = 0;
+    // the reference's overflow counters (counters.hip): per (view, entry)
+    // flags, summed on the device after the last view
+    const bool want_counts = bw != BIT_WIDTH_64 && E > 0 && V > 0;
+    bool counted = false;
+    if (want_counts) {
+        if (D.flags_cap < V * E) {
+            dfree(D.d_flags);
+            check(hipMalloc((void**)&D.d_flags, V * E), "overflow flags");
+            D.flags_cap = V * E;
+        }
+        check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe, D.stream), "memset");
+    }
     // single query view and a small k: only heap-changing candidates come back
     const double t_prep0 = now_ms();
     double prep = 0, sync_wait = 0;
@@ -718,7 +743,16 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     if (ind && !(out.sparse && V > 1 && V <= kMaxBatchPipe)) fatal("device_search: batch not pipelinable");
     const bool multi = out.sparse && V > 1 && !ind;
     const bool piped = multi || ind;
-    const size_t ovf_capv = piped ? kOvfCap / V - 1 : kOvfCap;
+    // every lane fits a view's overflow list (reference: no limit on the
+    // sequences search_16.c:101-109 re-runs at 64 bits)
+    const size_t ovf_capv = std::max<size_t>((size_t)D.ngroups * 64, 1);
+    if (D.ovf_slices < (piped ? V : 1)) {
+        dfree(D.d_ovf);
+        dfree(D.d_wide);
+        D.ovf_slices = piped ? V : 1;
+        check(hipMalloc((void**)&D.d_ovf, D.ovf_slices * (ovf_capv + 1) * 4), "overflow list");
+        check(hipMalloc((void**)&D.d_wide, D.ovf_slices * ovf_capv * 8), "wide scores");
+    }
     // pipelined: per-query candidate regions (device and pinned host)
     const size_t dreg = ind ? ((size_t)kFilterHeader * 4 + E * 8 + 255) & ~(size_t)255 : 0;
     const size_t hreg = (size_t)kFilterHeader * 4 + D.h_cand_cap * 8;
@@ -792,9 +826,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         int32_t* hs = D.h_scores + v * E;
         if (E == 0) continue;
         if (m == 0) {
-            // no query rows: SW scores 0, NW the boundary value H(-1, n-1)
+            // no query rows: SW scores 0, NW the boundary value H(-1, n-1);
+            // the reference skips the pair (no overflow)
             for (size_t e = 0; e < E; e++)
                 hs[e] = nw ? (int32_t)(Q + (int64_t)D.meta.len[e] * R) : 0;
+            if (want_counts) check(hipMemsetAsync(D.d_flags + v * E, 0, E, D.stream), "memset");
             continue;
         }
         // profile bounds over the residue codes the DB holds
@@ -809,6 +845,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (A == 0) minM = maxM = 0;
         const bool fits16 = minM >= -32768 && maxM <= 32767;
         uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(m, Q, R, minM, maxM) : 0xffffffffu) : 0;
+        // SW with a positive gap increment (R > 0 or Q + R > 0): E would keep
+        // growing through the strip kernels' padding columns past an entry's
+        // end and leak into its maximum -- every lane goes to the exact int64
+        // kernel (the reference's full_sw recurrence)
+        if (!nw && (R > 0 || Q + R > 0)) nmax16 = 0;
         if (C.force_wide) nmax16 = 0;
         // SW on f16 bit patterns needs non-positive gaps and scores within
         // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
@@ -934,7 +975,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         // device upload block: [matrix 8 KB][top boundary][query codes]
         const size_t top_bytes = (top.size() * 4 + 15) & ~(size_t)15;
-        const size_t blk_bytes = 8192 + top_bytes + m;
+        const size_t blk_bytes = kUpHeader + top_bytes + m;
         const size_t up_bytes = blk_bytes + 16 + qpt.size() * 4;
         // the staging buffer is reused: in a multi-view search the previous
         // view's copies may still be queued behind its predecessor's kernel
@@ -950,8 +991,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMalloc((void**)&D.d_upblk, D.upblk_cap), "per-search uploads");
         }
         D.d_matrix = (int64_t*)D.d_upblk;
-        D.d_top = (uint32_t*)(D.d_upblk + 8192);
-        D.d_query = D.d_upblk + 8192 + top_bytes;
+        D.d_top = (uint32_t*)(D.d_upblk + kUpHeader);
+        D.d_query = D.d_upblk + kUpHeader + top_bytes;
         // one pinned staging buffer for the per-search uploads (pageable
         // sources would make each copy a synchronous staged transfer)
         if (D.h_up_cap < up_bytes) {
@@ -961,10 +1002,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         // staging mirrors the device block, then the strip kernels' table
         uint8_t* up_m = D.h_up;
-        uint8_t* up_t = up_m + 8192;
+        uint8_t* up_t = up_m + kUpHeader;
         uint8_t* up_s = up_t + top_bytes;
         uint8_t* up_q = D.h_up + ((blk_bytes + 15) & ~(size_t)15);
         memcpy(up_m, Mc, 1024 * 8);
+        for (int y = 0; y < 32; y++) memcpy(up_m + 8192 + 8 * y, &M[y], 8);   // code 0's row, M[0][y]
         if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_s, qv.seq, m);
         if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
@@ -1089,6 +1131,60 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (long_groups > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
         check(hipEventRecord(ev_k1, st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
+        if (want_counts) {
+            // 8/16-bit overflow flags of this view's lanes (counters.hip);
+            // "ordinary" widths are decided from exact values and bounds
+            int64_t lo = minM, hi = maxM, pm = INT64_MIN;
+            for (size_t i = 0; i < m; i++) {
+                const int64_t x = M[qv.seq[i]];           // padding code 0
+                lo = std::min(lo, x);
+                hi = std::max(hi, x);
+                pm = std::max(pm, x);
+            }
+            int ordinary = 0;
+            for (int b = 0; b < 2; b++) {
+                const int64_t imin = b ? -32768 : -128, imax = b ? 32767 : 127;
+                const bool ok = Q <= 0 && R <= 0 && Q + R >= imin && (!nw || Q + R <= -1) && lo >= imin && hi <= imax;
+                ordinary |= (int)ok << b;
+            }
+            FlagArgs fa{};
+            fa.res = D.d_res;
+            fa.groups = D.d_groups;
+            fa.lane_len = D.d_lane_len;
+            fa.lane_out = D.d_lane_out;
+            fa.scores = a.scores;
+            fa.query = D.d_query;
+            fa.matrix = D.d_matrix;
+            fa.padrow = (const int64_t*)(D.d_upblk + 8192);
+            fa.flags = D.d_flags + v * E;
+            fa.list = D.d_flist;
+            fa.work = (int32_t*)D.d_work;
+            fa.nlanes = D.ngroups * 64;
+            fa.m = (uint32_t)m;
+            fa.threads = wide_threads;
+            fa.gap_open = Q;
+            fa.gap_extend = R;
+            fa.nw = nw ? 1 : 0;
+            fa.widths = bw == BIT_WIDTH_8 ? 3 : 2;
+            fa.ordinary = ordinary;
+            fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
+            fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
+            check(launch_flags(fa, st), "overflow flags launch");
+            if (ind || v + 1 == V) {
+                // a batch query's own counters, or the search's over all views
+                CountArgs ca{};
+                ca.flags = ind ? fa.flags : D.d_flags;
+                ca.entries = (uint32_t)E;
+                ca.views = ind ? 1u : (uint32_t)V;
+                ca.bw = bw;
+                ca.out = D.d_cnt + (ind ? 2 * v : 0);
+                check(launch_count(ca, st), "overflow count launch");
+                if (v + 1 == V)
+                    check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st),
+                          "D2H counters");
+                counted = v + 1 == V;
+            }
+        }
         kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
         if (ind) {
             // this query's own filter pass into its own candidate region
@@ -1099,8 +1195,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             f.n = (uint32_t)E;
             f.k = (uint32_t)k;
             f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
-            f.nw = nw ? 1 : 0;
-            f.bw = bw;
             f.summary = D.d_summary;
             f.thresh = D.d_thresh;
             f.thresh_local = D.d_thresh_local;
@@ -1125,8 +1219,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             f.n = (uint32_t)(multi ? V * E : E);
             f.k = (uint32_t)k;
             f.nblocks = (uint32_t)((f.n + kFilterBlock - 1) / kFilterBlock);
-            f.nw = nw ? 1 : 0;
-            f.bw = bw;
             f.summary = D.d_summary;
             f.thresh = D.d_thresh;
             f.thresh_local = D.d_thresh_local;
@@ -1143,8 +1235,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                   "D2H candidates");
         } else {
             check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
-            check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * 4097, hipMemcpyDeviceToHost, st), "D2H overflow");
-            check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * 4096, hipMemcpyDeviceToHost, st), "D2H wide");
+            // (the first kOvfPinned entries; d_ovf holds ovf_capv + 1 dwords)
+            const size_t pre = std::min(kOvfPinned, ovf_capv);
+            check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * (pre + 1), hipMemcpyDeviceToHost, st), "D2H overflow");
+            check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * pre, hipMemcpyDeviceToHost, st), "D2H wide");
         }
         check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
@@ -1159,16 +1253,27 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         // exact int64 scores of overflowed lanes: view vv's list and scores
         auto take_wide = [&](size_t vv, uint32_t nov, SearchScores& dst, size_t key_view) {
-            if (nov > ovf_capv) fatal("overflow list exhausted (%u entries)", nov);
             const uint32_t* ov = D.d_ovf + (piped ? vv * (ovf_capv + 1) : 0);
             const int64_t* wd = D.d_wide + (piped ? vv * ovf_capv : 0);
-            if (out.sparse || nov > 4096) {
+            const uint32_t* hov = D.h_ovf;
+            const int64_t* hwd = D.h_wide;
+            std::vector<uint32_t> big_ovf;
+            std::vector<int64_t> big_wide;
+            if (nov > kOvfPinned) {
+                big_ovf.resize((size_t)nov + 1);
+                big_wide.resize(nov);
+                check(hipMemcpy(big_ovf.data(), ov, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
+                check(hipMemcpy(big_wide.data(), wd, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
+                hov = big_ovf.data();
+                hwd = big_wide.data();
+            } else if (out.sparse) {
                 check(hipMemcpy(D.h_ovf, ov, 4 * ((size_t)nov + 1), hipMemcpyDeviceToHost), "D2H overflow");
                 check(hipMemcpy(D.h_wide, wd, 8 * (size_t)nov, hipMemcpyDeviceToHost), "D2H wide");
             }
+            dst.wide.reserve(dst.wide.size() + nov);
             for (uint32_t i = 0; i < nov; i++) {
-                const uint32_t e = D.lane_out[D.h_ovf[1 + i]];
-                dst.wide[(uint64_t)key_view * E + e] = D.h_wide[i];
+                const uint32_t e = D.lane_out[hov[1 + i]];
+                dst.wide[(uint64_t)key_view * E + e] = hwd[i];
             }
             wide_total += nov;
         };
@@ -1196,8 +1301,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                     D.h_scores[vv * E + cand[i].x] = (int32_t)cand[i].y;
                 }
                 std::sort(o.cand.begin(), o.cand.end());
-                o.dev_o8 = hf[1];
-                o.dev_o16 = hf[2];
+                o.dev_o8 = want_counts ? D.h_cnt[2 * vv] : 0;
+                o.dev_o16 = want_counts ? D.h_cnt[2 * vv + 1] : 0;
                 if (hf[3]) take_wide(vv, hf[3], o, 0);
                 o.kernel = kname;
             }
@@ -1220,8 +1325,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 out.cand[i] = x;
                 D.h_scores[x] = (int32_t)cs[i].y;
             }
-            out.dev_o8 += D.h_fbuf[1];
-            out.dev_o16 += D.h_fbuf[2];
             for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
                 const uint32_t nov = D.h_fbuf[3 + vv];
                 if (nov) take_wide(multi ? vv : v, nov, out, multi ? vv : v);
@@ -1244,7 +1347,25 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         wms += t;
         check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
         dms += t;
+        if (counted && !ind) {
+            out.dev_o8 = D.h_cnt[0];
+            out.dev_o16 = D.h_cnt[1];
+        }
         if (trace_on()) fprintf(stderr, "trace: post-sync %.3f\n", now_ms() - t_post0);
+    }
+    if (want_counts && !counted) {
+        // the last view had no query rows: sum the flags now
+        CountArgs ca{};
+        ca.flags = D.d_flags;
+        ca.entries = (uint32_t)E;
+        ca.views = (uint32_t)V;
+        ca.bw = bw;
+        ca.out = D.d_cnt;
+        check(launch_count(ca, D.stream), "overflow count launch");
+        check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16, hipMemcpyDeviceToHost, D.stream), "D2H counters");
+        check(hipStreamSynchronize(D.stream), "counters");
+        out.dev_o8 = D.h_cnt[0];
+        out.dev_o16 = D.h_cnt[1];
     }
     if (trace_on())
         fprintf(stderr, "trace: prep %.3f sync %.3f total %.3f\n", prep, sync_wait, now_ms() - t_prep0);

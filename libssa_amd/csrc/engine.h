@@ -50,10 +50,13 @@ struct DeviceDB {
     int32_t* d_scores = nullptr;
     int32_t* h_scores = nullptr;          // pinned, [views][entries]
     size_t h_scores_cap = 0;
-    uint32_t* d_ovf = nullptr;            // [0] = count, [1..] = list
-    uint32_t* h_ovf = nullptr;            // pinned
+    // overflow lists: per view slice [0] = count, [1..lanes] = lanes to re-score
+    // exactly (room for every lane: no cap), their int64 scores in d_wide
+    uint32_t* d_ovf = nullptr;
     int64_t* d_wide = nullptr;
-    int64_t* h_wide = nullptr;            // pinned
+    size_t ovf_slices = 0;                // view slices d_ovf / d_wide hold
+    uint32_t* h_ovf = nullptr;            // pinned, kOvfPinned + 1
+    int64_t* h_wide = nullptr;            // pinned, kOvfPinned
     uint32_t* d_qpt = nullptr;
     size_t qpt_cap = 0;
     size_t scores_cap = 0;                // d_scores entries
@@ -76,6 +79,13 @@ struct DeviceDB {
     int64_t* d_matrix = nullptr;
     int64_t* d_work = nullptr;
     size_t work_cap = 0;
+    // the reference's 8/16-bit overflow counters (counters.hip): per (view,
+    // entry) flags, the replay's lane list, per-query (o8, o16) sums
+    uint8_t* d_flags = nullptr;
+    size_t flags_cap = 0;
+    uint32_t* d_flist = nullptr;          // [0] count, then up to ngroups * 64 lanes
+    unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
+    unsigned long long* h_cnt = nullptr;  // pinned mirror
     // long entries (long_kernel, launched on stream_long beside the pair
     // kernel): the groups' column counts (longest first), their sum, the
     // device's SIMD count, the multi-pass scratch

@@ -95,15 +95,14 @@ struct FilterArgs {
     const uint32_t* order;     // [n] score index of insertion position p (null: identity) -- the
                                // chunk-interleaved order of multi-view searches
     uint32_t n, k, nblocks;
-    int32_t nw, bw;            // counters follow the reference's overflow rules
-    int32_t* summary;          // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
+    int32_t* summary;         // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
     int32_t* thresh;           // [nblocks] bound from earlier blocks
     int32_t* thresh_local;     // [nblocks * 64] bound from earlier minis of the same block
     int32_t* before;           // [nblocks][kFilterMaxK] scan scratch
     const uint32_t* ovf_count; // view v's count at ovf_count[v * ovf_stride], copied into counters[3 + v]
     uint32_t ovf_stride, nviews;
-    uint32_t* counters;        // [0] candidates, [1] 8-bit overflows, [2] 16-bit overflows,
-                               // [3 + v] overflowed lanes of view v (one host copy fetches everything)
+    uint32_t* counters;        // [0] candidates, [3 + v] overflowed lanes of view v
+                               // (one host copy fetches everything)
     uint2* cand;               // [n] (insertion position, score) of the candidates, unordered;
                                // at counters + kFilterHeader
 };
@@ -118,6 +117,48 @@ hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 // rl: rows per lane (4, 8, 12 or 16; 64*rl rows per pass)
 hipError_t launch_long(const LongArgs& a, int rl, bool nw, hipStream_t st);
 size_t long_lds_bytes(uint32_t alpha, int rl);
+
+// The reference's 8/16-bit overflow counters (counters.hip).  m_run reports
+// how many (query view, DB sequence) pairs its w-bit SIMD kernels sent on to
+// the next width (manager.c:157-160, search_8.c:94-124, search_16.c:92-114);
+// the scores here are exact at every width, so whether the reference's
+// saturated w-bit run would have overflowed is decided per lane: from the
+// exact score and bounds where that is provable (flags_decide_kernel), else
+// by replaying the reference's saturated w-bit recurrence for that lane
+// (flags_replay_kernel).  Per (view, entry) flag byte: bit 0 = 8-bit
+// overflow, bit 1 = 16-bit overflow.
+struct FlagArgs {
+    const uint4* res;
+    const GroupDesc* groups;
+    const uint32_t* lane_len;
+    const uint32_t* lane_out;
+    const int32_t* scores;     // this view's exact scores (INT32_MIN: value elsewhere -> replay)
+    const uint8_t* query;      // [m]
+    const int64_t* matrix;     // [1024] compact code x query code
+    const int64_t* padrow;     // [32] M[0][y]: the reference pads a sequence to 4 columns with code 0
+    uint8_t* flags;            // this view's [entries]
+    uint32_t* list;            // [0] count, [1..nlanes] lanes left to the replay
+    int32_t* work;             // replay scratch, [2m][threads] (thread-interleaved)
+    uint32_t nlanes, m, threads;
+    int32_t gap_open, gap_extend;
+    int32_t nw;
+    int32_t widths;            // bit 0: 8-bit flags wanted, bit 1: 16-bit
+    int32_t ordinary;          // bit 0/1: 8/16-bit decidable from exact values (host-checked regime)
+    int32_t maxm;              // max(0, M over the DB's codes and code 0 x the query's residues)
+    int32_t padmax;            // max(0, max_i M[0][q_i])
+};
+hipError_t launch_flags(const FlagArgs& a, hipStream_t st);
+
+// counters of one search: out[0] += sum_e a8(e), out[1] += width 8 ?
+// sum_e a8(e) * a16(e) : sum_e a16(e), a_w(e) = #views whose flag w is set
+// (oracle_overflow_counts restates it)
+struct CountArgs {
+    const uint8_t* flags;      // [views][entries]
+    uint32_t entries, views;
+    int32_t bw;
+    unsigned long long* out;   // [2]
+};
+hipError_t launch_count(const CountArgs& a, hipStream_t st);
 
 // pair_kernel's per-search pair tables, built on the device from the query
 // and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)

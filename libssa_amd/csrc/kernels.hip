@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "kernels.h"
@@ -258,7 +259,7 @@ strip16_kernel(const StripArgs a) {
     }
     if (ovf) {
         const uint32_t idx = atomicAdd(a.ovf_count, 1u);
-        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;   // host aborts when the count exceeds the cap
+        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;   // (the list has room for every lane)
         a.scores[o] = INT32_MIN;
     } else {
         a.scores[o] = score;
@@ -917,30 +918,15 @@ constexpr int kMinisPerBlock = kFilterBlock / kMini;   // 64
 
 __global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
     __shared__ int32_t mini_max[kMinisPerBlock];
-    __shared__ uint32_t c8, c16;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * kFilterBlock;
-    if (threadIdx.x == 0) c8 = c16 = 0;
-    __syncthreads();
-    uint32_t my8 = 0, my16 = 0;
     for (int i = 0; i < kMinisPerBlock / 4; i++) {
         const int m = i * 4 + wave;                 // this wave's mini: 64 consecutive entries
         const uint32_t e = base + m * kMini + lane;
         const int32_t x = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
-        if (x != INT32_MIN) {
-            if (!a.nw) {
-                my8 += a.bw == 8 && x >= 255;
-                my16 += x >= 65535;
-            } else {
-                my8 += a.bw == 8 && (x <= -128 || x >= 127);
-                my16 += x <= -32768 || x >= 32767;
-            }
-        }
         const int32_t mx = wave_max(x);
         if (lane == 0) mini_max[m] = mx;
     }
-    if (my8) atomicAdd(&c8, my8);
-    if (my16) atomicAdd(&c16, my16);
     __syncthreads();
     if (wave == 0) {
         const int K = (int)a.k;
@@ -953,10 +939,6 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
         }
         a.thresh_local[(size_t)blockIdx.x * kMinisPerBlock + lane] = tl;
         a.summary[(size_t)blockIdx.x * kFilterMaxK + lane] = lane < K ? run : INT32_MIN;
-        if (lane == 0) {
-            if (c8) atomicAdd(&a.counters[1], c8);
-            if (c16) atomicAdd(&a.counters[2], c16);
-        }
     }
 }
 
@@ -1241,15 +1223,24 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
 
 size_t long_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * rl * 2; }
 
+// hipFuncSetAttribute (dynamic LDS above 64 KiB) once per kernel and device:
+// the per-device search threads of a multi-GPU search launch concurrently
+static hipError_t lds_attr_once(const void* fn, std::atomic<uint64_t>& done, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
+
 template <int RL, bool NW>
 static hipError_t launch_long_t(const LongArgs& a, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)long_kernel<RL, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)long_lds_bytes(32, 16));
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t e = lds_attr_once((const void*)long_kernel<RL, NW>, attr, (int)long_lds_bytes(32, 16));
+    if (e != hipSuccess) return e;
     const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
     hipLaunchKernelGGL((long_kernel<RL, NW>), dim3(blocks), dim3(64 * kLongWaves), long_lds_bytes(a.alpha, RL), st, a);
     return hipGetLastError();
@@ -1293,13 +1284,9 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
 
 template <int NP, bool NW, int NPT>
 static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pair_kernel<NP, NW, NPT>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLdsMax);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t e = lds_attr_once((const void*)pair_kernel<NP, NW, NPT>, attr, (int)kPairLdsMax);
+    if (e != hipSuccess) return e;
     constexpr int W = pair_waves(NP, NW);
     const uint32_t blocks = (a.ngroups - a.g_first + W - 1) / W;
     hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);

@@ -58,7 +58,90 @@ def test_kat_public_api(case, width):
     for algo, fn in (("sw", S.sw_align), ("nw", S.nw_align)):
         got = [(h["score"], h["id"]) for h in fn(q, case["k"], width)]
         assert got == [tuple(x) for x in case[algo + "_64"]], (algo, got[:5])
+        # m_run's overflow counters (manager.c:157-160) as the reference's own
+        # 8/16-bit runs report them (tests/golden/kat.json from the harness;
+        # incl. overflow_127 1/1, sw_overflow_534 1/0, test.fas NW int8 4/0)
+        st = S.stats()
+        exp = {S.BIT_WIDTH_8: tuple(case[algo + "_8_overflow"]), S.BIT_WIDTH_16: (0, case[algo + "_16_overflow"]),
+               S.BIT_WIDTH_64: (0, 0)}[width]
+        assert (st["overflow_8"], st["overflow_16"]) == exp, (algo, width)
     S.free_sequence(q)
+
+
+OVF = np.load(os.path.join(GOLDEN, "overflow.npz"))
+OVF_CASES = json.loads(str(OVF["meta"]))
+
+
+@pytest.mark.parametrize("case", OVF_CASES, ids=[f"c{c['id']}" for c in OVF_CASES])
+def test_overflow_counters_vs_reference_flags(case, tmp_path):
+    """The reference's per-sequence 8/16-bit overflow flags (its own SIMD
+    kernels, tools/gen_golden.py gen_overflow) summed the way m_run does
+    equal ssa_amd_get_stats' counters at widths 8 and 16 -- ordinary and
+    pathological (wrapping, zero, positive) gap penalties, SW and NW; the
+    scores are checked against the oracle at every width too."""
+    t = case["id"]
+    q, db, off = OVF[f"c{t}_q"], OVF[f"c{t}_db"], OVF[f"c{t}_off"]
+    flags = OVF[f"c{t}_flags"]
+    if case["matrix"] == "const":
+        spec = ("const", case["match"], case["mismatch"])
+        M = po.matrix_constant(case["match"], case["mismatch"])
+    else:
+        spec = ("builtin", case["matrix"])
+        M = TABLES["matrices"][NAMES.index(case["matrix"])].copy()
+    configure(False, spec, case["gap_open"], case["gap_extend"])
+    S.init_db(_write_db(str(tmp_path), db, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    seqs = [db[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    exp_hits = po.search(case["algo"], q, seqs, M, case["gap_open"], case["gap_extend"], 5)
+    fn = S.nw_align if case["algo"] else S.sw_align
+    for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
+        got = [(h["score"], h["id"]) for h in fn(qq, 5, width)]
+        assert got == exp_hits, width
+        st = S.stats()
+        o8, o16 = po.overflow_counts(width, flags)
+        assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_overflow_counters_two_views(algo, tmp_path):
+    """NUCLEOTIDE with both strands: 2 query views x 2 DB strands per record.
+    Width 8's 16-bit count is sum_e a8(e) * a16(e) -- the 8-bit overflow
+    chunk holds an entry once per overflowing view and search_16_chunk re-runs
+    every copy for every view (search_8.c:94-124) -- against the oracle's
+    replays of the reference's saturated kernels (oracle_overflow_counts)."""
+    rng = np.random.default_rng(5 + algo)
+    q = syn.dna_query(1500, 3)
+    seqs = []
+    for i in range(80):
+        n = int(rng.integers(20, 700))
+        if i % 5 == 0:
+            st0 = int(rng.integers(0, len(q) - n + 1))
+            seqs.append(q[st0:st0 + n].copy())
+        else:
+            seqs.append(rng.choice(syn.NT_ACGT, n).astype(np.uint8))
+    db, off = po.pack_db(seqs)
+    configure(True, ("const", 127, -1), -1, -1, strands=S.BOTH_STRANDS)
+    S.init_db(_write_db(str(tmp_path), db, off, nucleotide=True))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=True))
+    views = [np.frombuffer(v[0], np.uint8) for v in S.query_views(qq)]
+    assert len(views) == 2
+    comp = np.zeros(32, np.uint8)
+    comp[views[0]] = views[1][::-1]
+    entries = []
+    for x in seqs:
+        entries += [x, comp[x[::-1]]]
+    edb, eoff = po.pack_db(entries)
+    M = po.matrix_constant(127, -1)
+    flags = np.stack([po.overflow_flags(algo, v, edb, eoff, M, -1, -1) for v in views])
+    fn = S.nw_align if algo else S.sw_align
+    for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
+        fn(qq, 5, width)
+        st = S.stats()
+        o8, o16 = po.overflow_counts(width, flags)
+        assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    assert po.overflow_counts(8, flags)[1] > 0        # the product term is exercised
+    S.free_sequence(qq)
 
 
 @pytest.mark.parametrize("np_", [8, 16, 32])
@@ -917,3 +1000,87 @@ def test_gap_penalty_edges_vs_oracle(gaps, algo):
             assert (sc == exp).all(), (pnp, np.nonzero(sc != exp)[0][:10])
         S.set_option("pair_np", 24)
         S.free_sequence(qq)
+
+
+# ------------------------------------------------ full-size reference pins
+FULL = json.load(open(os.path.join(GOLDEN, "fullsize.json")))
+
+
+def _fullsize_inputs(c):
+    """The FULLSIZE DBs of tools/gen_golden.py, regenerated from the same
+    block-seeded generators (a share = the first IDs of the whole DB)."""
+    if c["kind"] == "dna":
+        q = syn.dna_query(c["qlen"], c["qseed"])
+        codes, off = syn.dna_reads_range(c["n"], c["seed"], 0, c["i1"], 150, query=q)
+        return q, codes, off
+    q = syn.protein_query(c["qlen"], c["qseed"])
+    codes, off = syn.protein_db_range(c["n"], c["seed"], 0, c["i1"], query=q, alphabet=c.get("alphabet", "bg20"),
+                                      lengths=c.get("lengths", "gamma"), lo=c.get("lo", 16), hi=c.get("hi", 4096))
+    return q, codes, off
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_fullsize_matches_reference_hash(name, tmp_path):
+    """BASELINE.json's configurations at full size (C2, C3: 1 M sequences) or
+    one GPU's share (C4: the first 1.25 M of the 10 M DB at width 8; C5: the
+    first 1 M of the 50 M reads, q = 10 000 nt), plus 25- and 28-symbol
+    alphabets: the SHA-256 of the full int64 score vector in ID order, the
+    score histogram, the top-1/10/64 and m_run's overflow counters equal the
+    reference's own 16/8-bit AVX2 search of the same DB
+    (tests/golden/fullsize.json, tools/gen_golden.py fullsize)."""
+    c = FULL[name]
+    q, codes, off = _fullsize_inputs(c)
+    n = len(off) - 1
+    dna = c["kind"] == "dna"
+    if c["matrix"].startswith("const"):
+        a, b = c["matrix"][5:].split("_")
+        spec = ("const", int(a), int(b))
+    else:
+        spec = ("builtin", c["matrix"])
+    configure(dna, spec, c["gap_open"], c["gap_extend"])
+    path = os.path.join(str(tmp_path), "db.fas")
+    syn.write_fasta(path, codes, off, dna)
+    del codes
+    S.init_db(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
+    algo = S.SW if c["algo"] == "sw" else S.NW
+    # k = n: every entry is inserted, so the log is the full score vector
+    log = S.search(qq, algo, n, c["width"], S.LOG, cap=n + 8)
+    st = S.stats()
+    assert [st["overflow_8"], st["overflow_16"]] == c["overflow"]
+    assert len(log) == n
+    arr = np.array([(h[1], h[0]) for h in log], dtype=np.int64)
+    arr = arr[np.argsort(arr[:, 0], kind="stable")]
+    assert (arr[:, 0] == np.arange(n)).all()
+    sc = arr[:, 1]
+    vals, counts = np.unique(sc, return_counts=True)
+    assert vals.tolist() == c["hist_values"] and counts.tolist() == c["hist_counts"]
+    assert hashlib.sha256(sc.astype("<i8").tobytes()).hexdigest() == c["sha256"]
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    for k in (1, 10, 64):
+        got = [[h["score"], h["id"]] for h in fn(qq, k, c["width"])]
+        assert got == c[f"top{k}"], k
+        st = S.stats()
+        assert [st["overflow_8"], st["overflow_16"]] == c["overflow"], k
+    S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("gaps", [(-11, 2), (3, -1)])
+def test_every_lane_rescored_exactly(gaps, tmp_path):
+    """SW with a positive gap increment sends every lane to the exact int64
+    kernel (no cap on the overflow list: more entries than the pinned
+    mirror holds); scores and top-k equal the oracle's full_sw, which runs
+    the reference recurrence with the same penalties."""
+    q = syn.protein_query(60, 11)
+    codes, off = syn.protein_db(6000, 9, query=q, plant_every=700, lo=5, hi=120)
+    configure(False, ("builtin", "blosum62"), gaps[0], gaps[1])
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    exp = po.scores(0, q, codes, off, M, gaps[0], gaps[1])
+    got, ids = _full_scores(qq, S.SW, len(off) - 1)
+    assert (got == exp).all()
+    seqs = [codes[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    assert [(h["score"], h["id"]) for h in S.sw_align(qq, 20, 16)] == po.search(0, q, seqs, M, gaps[0], gaps[1], 20)
+    assert S.stats()["wide_count"] == len(off) - 1
+    S.free_sequence(qq)
