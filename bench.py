@@ -76,6 +76,13 @@ def parse():
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
     p.add_argument("--pair-np", type=int, default=24, help="pair kernel main strip: 24 (48 rows) or 16 (32 rows)")
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
+    p.add_argument("--alphabet", default="bg20", choices=["bg20", "sprot25", "uniform28"],
+                   help="protein residue set: 20 standard (BLOSUM62 background), Swiss-Prot-like 25 "
+                        "(+X,B,Z,U,O), the reference generator's uniform 28 (generate_db.c:117-118)")
+    p.add_argument("--lengths", default="gamma", choices=["gamma", "uniform"],
+                   help="protein lengths: 1+Gamma(2,175) in [16,4096], or uniform [16,1000) like generate_db.c")
+    p.add_argument("--torch-gather", action="store_true",
+                   help="N>1: gather the shard logs with torch.distributed instead of ssa_amd_gather_logs")
     args = p.parse_args()
     cfg = CONFIGS[args.config]
     for key in ("qlen", "algo", "matrix", "gap_open", "gap_extend"):
@@ -124,25 +131,64 @@ def matrix_table(name):
     return tabs["matrices"][[str(x) for x in tabs["names"]].index(name)].copy()
 
 
-def cpu_baseline(codes, off, q, M, args, cores):
+def host_cpu():
+    """(threads to use, description) of the host's CPU share: the affinity
+    mask, capped by the cgroup CPU quota and OMP_NUM_THREADS when set (the GPU
+    box exports the box's share there), plus the CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    n, notes = aff, [f"affinity {aff}"]
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            qc = max(1, -(-int(quota) // int(period)))
+            n = min(n, qc)
+            notes.append(f"cgroup quota {qc}")
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+        notes.append(f"OMP_NUM_THREADS {omp}")
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model, ", ".join(notes)
+
+
+def cpu_baseline(codes, off, q, M, args):
     """The reference's own AVX2 int16 kernel (search_16_chunk ->
     search_16_avx2_sw, compiled from its sources into oracle/_ref) timed on
-    the host cores over a bounded sample; falls back to the int64 oracle
-    port when the reference build is absent."""
+    the host's CPU share (every core of it) over a bounded sample, and on one
+    thread; falls back to the int64 oracle port when the reference build is
+    absent."""
     from oracle import pyoracle as po
+    cores, model, share = host_cpu()
     algo = 0 if args.algo == "sw" else 1
     n = len(off) - 1
     if po.have_ref():
-        # size the sample to ~cpu_seconds at a conservative 8 GCUPS/thread
         cells_per_seq = float(off[-1]) / n * len(q)
-        sample = int(min(n, max(1000, args.cpu_seconds * 8e9 * cores / cells_per_seq)))
-        soff = off[:sample + 1]
-        hits, _, ns, secs = po.ref_run(po.MODE_SEARCH16_AVX2, algo, q, None, M, args.gap_open, args.gap_extend,
-                                       k=args.k, threads=cores, repeat=3, db_off=(codes, soff))
-        cells = float(soff[-1]) * len(q)
-        return {"value": cells / secs / 1e9, "unit": "GCUPS", "cores": cores, "kind": "reference",
+
+        def run(threads, seconds):
+            # sample sized to ~seconds at a conservative 8 GCUPS per thread
+            sample = int(min(n, max(1000, seconds * 8e9 * threads / cells_per_seq)))
+            soff = off[:sample + 1]
+            _, _, _, secs = po.ref_run(po.MODE_SEARCH16_AVX2, algo, q, None, M, args.gap_open, args.gap_extend,
+                                       k=args.k, threads=threads, repeat=2, db_off=(codes, soff))
+            cells = float(soff[-1]) * len(q)
+            return cells / secs / 1e9, sample, cells
+
+        v, sample, cells = run(cores, args.cpu_seconds * 0.6)
+        v1, sample1, _ = run(1, args.cpu_seconds * 0.3)
+        return {"value": v, "unit": "GCUPS", "cores": cores, "kind": "reference",
+                "one_thread_gcups": v1, "cpu_model": model, "host_share": share,
                 "sample": f"first {sample} of {n} DB sequences ({cells:.3g} cells), reference AVX2 int16 "
-                          f"search_16_chunk on {cores} threads, chunk 1000, k={args.k}"}
+                          f"search_16_chunk on {cores} threads (best of 2), chunk 1000, k={args.k}; one thread: "
+                          f"first {sample1} sequences"}
     po.build(quiet=True)
     sample = 2000
     soff = off[:sample + 1]
@@ -150,8 +196,35 @@ def cpu_baseline(codes, off, q, M, args, cores):
     po.scores(algo, q, codes[:int(soff[-1])], soff, M, args.gap_open, args.gap_extend, threads=cores)
     secs = time.perf_counter() - t0
     cells = float(soff[-1]) * len(q)
-    return {"value": cells / secs / 1e9, "unit": "GCUPS", "cores": cores, "kind": "port",
-            "sample": f"first {sample} DB sequences, oracle int64 scalar port on {cores} threads"}
+    return {"value": cells / secs / 1e9, "unit": "GCUPS", "cores": cores, "kind": "port", "cpu_model": model,
+            "host_share": share, "sample": f"first {sample} DB sequences, oracle int64 scalar port on {cores} threads"}
+
+
+def make_shard(args, cfg, rank, world):
+    """This rank's contiguous ID slice of the config's synthetic DB, from the
+    block-seeded generators (libssa_amd/synthetic.py: a slice is
+    byte-identical to the same IDs of the whole DB).  Weak configs (C2/C3/ref):
+    an N x seqs DB, 1 M per rank; strong ones (C4/C5): the fixed 10 M / 50 M DB
+    cut into N ID ranges, so every N searches the same DB.  At N = 1 C2 and C3
+    are exactly tests/golden/fullsize.json's c2/c3 DBs.
+    Returns (query, codes, offsets, first global ID, DB size)."""
+    from libssa_amd import synthetic as syn
+    if args.seqs is not None or cfg["total_seqs"] is None:
+        per = args.seqs if args.seqs is not None else cfg["seqs"]
+        total = per * world
+    else:
+        total = cfg["total_seqs"]
+        per = (total + world - 1) // world
+    i0 = min(total, rank * per)
+    i1 = min(total, i0 + per)
+    if args.db == "dna":
+        q = syn.dna_query(args.qlen, 8)
+        codes, off = syn.dna_reads_range(total, 43, i0, i1, 150, query=q)
+        return q, codes, off, i0, total
+    q = read_query_file(cfg["query_file"]) if cfg.get("query_file") else syn.protein_query(args.qlen, 7)
+    codes, off = syn.protein_db_range(total, 42, i0, i1, query=q, alphabet=args.alphabet, lengths=args.lengths,
+                                      lo=16, hi=4096 if args.lengths == "gamma" else 1000)
+    return q, codes, off, i0, total
 
 
 def main():
@@ -192,21 +265,13 @@ def main():
     S.init_gap_penalties(args.gap_open, args.gap_extend)
     algo = S.SW if args.algo == "sw" else S.NW
     cfg = CONFIGS[args.config]
-    if args.seqs is None:
-        args.seqs = cfg["seqs"] if cfg["total_seqs"] is None else (cfg["total_seqs"] + world - 1) // world
 
     # --- synthetic shard (untimed): generate, write FASTA, pack into HBM
     t0 = time.time()
-    if dna:
-        q = syn.dna_query(args.qlen, 8)
-        codes, off = syn.dna_reads(args.seqs, 150, 43 + 1000 * rank, query=q, plant_every=100000)
-    else:
-        if cfg.get("query_file"):
-            q = read_query_file(cfg["query_file"])
-            args.qlen = len(q)
-        else:
-            q = syn.protein_query(args.qlen, 7)
-        codes, off = syn.protein_db(args.seqs, 42 + 1000 * rank, query=q, plant_every=10000, sampler="lut")
+    q, codes, off, id0, db_total = make_shard(args, cfg, rank, world)
+    args.qlen = len(q)
+    args.seqs = len(off) - 1
+    if not dna:
         if args.long_tail > 0:
             # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
             # residues); the others keep theirs
@@ -230,7 +295,7 @@ def main():
     gen_s = time.time() - t0
     t1 = time.time()
     S.init_db(path)
-    S.set_id_offset(rank * args.seqs)
+    S.set_id_offset(id0)
     S.prepare_db()
     os.remove(path)
     qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
@@ -238,12 +303,23 @@ def main():
     setup_s = time.time() - t0
     cells_local = float(off[-1]) * args.qlen
 
+    # N > 1: the shards' insertion logs meet on rank 0 in the library's own
+    # RCCL gather (ssa_amd_gather_logs); the RCCL unique id travels over the
+    # torch process group once
+    native = world > 1 and backend == "nccl" and not args.torch_gather
+    if native:
+        obj = [S.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        S.dist_init(rank, world, obj[0])
+
     def step():
         if world == 1:
             # the public sw_align / nw_align + free_alignment (libssa.h)
             return S.align_scores(qq, args.k, args.width, algo)
-        from libssa_amd.dist import global_topk
         log = S.search(qq, algo, args.k, args.width, S.LOG)
+        if native:
+            return S.gather_logs(log, args.k)
+        from libssa_amd.dist import global_topk
         return global_topk(log, args.k, dist, rank, world, dev)
 
     def sync():
@@ -276,6 +352,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st = S.stats()
+    if native:
+        S.dist_finalize()
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -317,7 +395,7 @@ def main():
         "config": {"workload": f"{args.config.upper()}: {args.algo.upper()} {args.matrix} gaps {args.gap_open}/{args.gap_extend}, "
                                f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
                                f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
-                   "db_seqs_per_gpu": args.seqs, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
+                   "db_seqs_per_gpu": args.seqs, "db_total_seqs": db_total, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
                    "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_np": args.pair_np, "strip_np": args.strip_np,
                    "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -340,13 +418,21 @@ def main():
         "setup": {"generate_and_write_fasta_s": round(gen_s, 1), "init_db_and_pack_s": round(load_s, 1),
                   "pack_ms": round(st["pack_ms"], 1)},
         "top_hit": list(res[0]) if res else None,
+        "gather": ("ssa_amd_gather_logs (RCCL)" if native else "torch.distributed") if world > 1 else None,
     }
+    # the same DB and query as a reference-pinned fixture: the step's top-k
+    # against the reference's own (tests/golden/fullsize.json)
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json"))).get(args.config)
+    if (fx and world == 1 and args.long_tail == 0 and args.alphabet == fx.get("alphabet", "bg20")
+            and args.lengths == fx.get("lengths", "gamma") and fx["n"] == db_total and fx["i1"] == args.seqs
+            and fx["qlen"] == args.qlen and fx["algo"] == args.algo and fx["gap_open"] == args.gap_open
+            and fx["gap_extend"] == args.gap_extend and fx["matrix"] == args.matrix and args.k in (1, 10, 64)):
+        out["topk_vs_reference"] = "match" if [list(x) for x in res] == fx[f"top{args.k}"] else "MISMATCH"
     if world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle as po
         M = matrix_table(args.matrix)
-        cores = min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(codes, off, q, M, args, cores)
+            out["cpu_baseline"] = cpu_baseline(codes, off, q, M, args)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     print(json.dumps(out))

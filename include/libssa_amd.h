@@ -104,6 +104,31 @@ size_t ssa_amd_search_batch( const p_query * queries, size_t nq, int algo, size_
  * writes the sorted top-k (score desc, id desc).  Returns the count. */
 size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );
 
+/* Multi-process search over RCCL (one process per GPU).  The
+ * reference merges its worker threads' heaps in one process
+ * (src/algo/manager.c:141-145); a sharded deployment merges the shards'
+ * insertion logs instead:
+ *   rank 0:        ssa_amd_dist_unique_id(id)   (id: ssa_amd_dist_unique_id_bytes()
+ *                  bytes, handed to the other ranks out of band -- MPI, a TCP
+ *                  store, a shared file)
+ *   every rank:    ssa_amd_set_device(local GPU); ssa_amd_dist_init(rank, world, id)
+ *   every search:  n = ssa_amd_search(q, algo, k, width, SSA_AMD_LOG, log, cap);
+ *                  c = ssa_amd_gather_logs(log, n, k, out)   (collective)
+ * ssa_amd_gather_logs gathers every rank's log over RCCL (one ncclAllGather
+ * of fixed 512-row slots; an exact-size ncclGather to rank 0 only when a log
+ * is longer) and on rank 0 writes the global sorted top-k to out and returns
+ * its length -- bit-identical to one process searching the whole DB; other
+ * ranks return 0.  ssa_amd_dist_init returns 0 on success.
+ * ssa_amd_merge_logs is rank 0's merge alone: nlogs logs at rows + r * stride
+ * (counts[r] rows each), replayed in order through the reference heap. */
+int ssa_amd_dist_unique_id( void * id );
+size_t ssa_amd_dist_unique_id_bytes( void );
+int ssa_amd_dist_init( int rank, int world, const void * id );
+void ssa_amd_dist_finalize( void );
+size_t ssa_amd_gather_logs( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );
+size_t ssa_amd_merge_logs( const ssa_hit_t * rows, const size_t * counts, size_t nlogs, size_t stride,
+                           size_t hitcount, ssa_hit_t * out );
+
 /* Persistent packed DB: ssa_amd_save_db writes the device
  * layout of the open DB (packing it first if needed); ssa_amd_load_db,
  * called after init_db on the same DB file and with the same

@@ -80,7 +80,9 @@ EXPORTS = {
                       "ssa_exit", "ssa_amd_device_count", "ssa_amd_set_device", "ssa_amd_set_id_offset",
                       "ssa_amd_prepare_db", "ssa_amd_get_stats", "ssa_amd_set_option", "ssa_amd_search",
                       "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
-                      "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch"],
+                      "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch",
+                      "ssa_amd_dist_unique_id", "ssa_amd_dist_unique_id_bytes", "ssa_amd_dist_init",
+                      "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -121,6 +123,11 @@ def load():
         "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
                                c_size_t),
         "ssa_amd_translate": ([c_int, c_char_p, c_size_t, c_int, c_int, c_char_p, c_size_t], c_size_t),
+        "ssa_amd_dist_unique_id": ([c_char_p], c_int), "ssa_amd_dist_unique_id_bytes": ([], c_size_t),
+        "ssa_amd_dist_init": ([c_int, c_int, c_char_p], c_int), "ssa_amd_dist_finalize": ([], None),
+        "ssa_amd_gather_logs": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
+        "ssa_amd_merge_logs": ([POINTER(ssa_hit_t), POINTER(c_size_t), c_size_t, c_size_t, c_size_t,
+                                POINTER(ssa_hit_t)], c_size_t),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -306,3 +313,57 @@ def search_batch(queries, algo, hitcount, bit_width=BIT_WIDTH_16):
     counts = (c_size_t * max(nq, 1))()
     L.ssa_amd_search_batch(qs, nq, algo, hitcount, bit_width, out, counts)
     return [[(out[i * hitcount + j].score, out[i * hitcount + j].db_id) for j in range(counts[i])] for i in range(nq)]
+
+
+# ---- multi-process gather over RCCL (libssa_amd.h ssa_amd_dist_*) ------------
+def dist_unique_id():
+    """Rank 0: the RCCL unique id (bytes) to hand to every rank."""
+    L = load()
+    buf = ctypes.create_string_buffer(L.ssa_amd_dist_unique_id_bytes())
+    if L.ssa_amd_dist_unique_id(buf) != 0:
+        raise RuntimeError("ssa_amd_dist_unique_id failed")
+    return buf.raw
+
+
+def dist_init(rank, world, uid):
+    if load().ssa_amd_dist_init(rank, world, uid) != 0:
+        raise RuntimeError(f"ssa_amd_dist_init({rank}, {world}) failed")
+
+
+def dist_finalize(): load().ssa_amd_dist_finalize()
+
+
+def _hit_array(log):
+    arr = (ssa_hit_t * max(len(log), 1))()
+    for i, h in enumerate(log):
+        arr[i].score, arr[i].db_id = int(h[0]), int(h[1])
+        if len(h) > 2:
+            arr[i].query_id, arr[i].db_strand, arr[i].db_frame = int(h[2]), int(h[3]), int(h[4])
+    return arr
+
+
+def gather_logs(log, hitcount):
+    """ssa_amd_gather_logs (collective): rank 0 gets the global sorted top-k
+    [(score, db_id)], the other ranks []."""
+    L = load()
+    arr = _hit_array(log)
+    out = (ssa_hit_t * max(hitcount, 1))()
+    c = L.ssa_amd_gather_logs(arr, len(log), hitcount, out)
+    return [(out[i].score, out[i].db_id) for i in range(c)]
+
+
+def merge_logs(logs, hitcount):
+    """ssa_amd_merge_logs: rank 0's merge of per-shard logs (in shard order)."""
+    L = load()
+    stride = max([len(x) for x in logs] + [1])
+    rows = (ssa_hit_t * (stride * max(len(logs), 1)))()
+    for r, lg in enumerate(logs):
+        for i, h in enumerate(lg):
+            rows[r * stride + i].score, rows[r * stride + i].db_id = int(h[0]), int(h[1])
+            if len(h) > 2:
+                rows[r * stride + i].query_id = int(h[2])
+                rows[r * stride + i].db_strand, rows[r * stride + i].db_frame = int(h[3]), int(h[4])
+    counts = (c_size_t * max(len(logs), 1))(*[len(x) for x in logs])
+    out = (ssa_hit_t * max(hitcount, 1))()
+    c = L.ssa_amd_merge_logs(rows, counts, len(logs), stride, hitcount, out)
+    return [(out[i].score, out[i].db_id) for i in range(c)]

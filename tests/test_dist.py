@@ -80,3 +80,38 @@ def test_shard_log_property():
         for a, b in ((0, 1000), (1000, 3333), (3333, 4000)):
             shards |= set(po.topk_log(sc[a:b], ids[a:b], k))
         assert glob <= shards
+
+
+@pytest.mark.parametrize("cuts", [[0, 4000], [0, 1000, 3333, 4000], [0, 0, 17, 2500, 2500, 4000]])
+@pytest.mark.parametrize("k", [1, 10, 300])
+def test_native_merge_logs_equals_single_process(cuts, k):
+    """ssa_amd_merge_logs -- rank 0's half of ssa_amd_gather_logs (csrc/dist.cpp)
+    -- over shard logs in shard order equals the single-process reference
+    heap, tie IDs included (tie-heavy scores, empty shards)."""
+    import libssa_amd as S
+    rng = np.random.default_rng(k)
+    sc = rng.integers(0, 40, 4000)
+    ids = np.arange(4000, dtype=np.uint64)
+    logs = [[(s, i, 0, 0, 0) for s, i in po.topk_log(sc[a:b], ids[a:b], k)] for a, b in zip(cuts, cuts[1:])]
+    assert S.merge_logs(logs, k) == po.topk(sc, ids, k)
+
+
+@pytest.mark.gpu
+def test_native_rccl_gather_world1(tmp_path):
+    """ssa_amd_dist_init + ssa_amd_gather_logs over RCCL with one rank (the
+    one-GPU box; the driver's 8-GPU run exercises N > 1): the fixed-slot
+    all-gather and the exact-size ncclGather round (a log longer than the
+    512-row slot) both return the replayed top-k."""
+    import libssa_amd as S
+    S.load()
+    S.set_device(0)
+    S.dist_init(0, 1, S.dist_unique_id())
+    try:
+        rng = np.random.default_rng(3)
+        for n, k in ((300, 10), (5000, 2000)):
+            sc = np.sort(rng.integers(0, 10 ** 6, n))       # rising: the log is the whole shard
+            ids = np.arange(n, dtype=np.uint64)
+            log = [(s, i, 0, 0, 0) for s, i in po.topk_log(sc, ids, k)]
+            assert S.gather_logs(log, k) == po.topk(sc, ids, k)
+    finally:
+        S.dist_finalize()
