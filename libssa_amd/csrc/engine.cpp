@@ -45,7 +45,9 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch);
-    dfree(d_flags); dfree(d_flist); dfree(d_cnt);
+    dfree(d_flags); dfree(d_flist); dfree(d_cnt); dfree(d_res_cls);
+    d_res_cls = nullptr;
+    cls_key.clear();
     if (h_cnt) (void)hipHostFree(h_cnt);
     d_flags = nullptr; d_flist = nullptr; d_cnt = nullptr; h_cnt = nullptr;
     flags_cap = 0;
@@ -833,12 +835,62 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (want_counts) check(hipMemsetAsync(D.d_flags + v * E, 0, E, D.stream), "memset");
             continue;
         }
+        // residue classes of this view: DB codes whose matrix rows agree on
+        // every residue of the query score identically, so the kernels may
+        // see one code per class.  Used when it lets more pair-kernel
+        // workgroups share a CU's LDS (the reference generator's uniform
+        // 28-symbol DB: '-', U, O and X score alike against a standard-residue
+        // query -> 25 classes, a 75.7 KiB table, two workgroups per CU instead
+        // of none); the class-coded residues are cached per class map.
+        const int pnp_v = C.pair_np == 24 ? 24 : 16;
+        std::vector<uint8_t> cls_of, cls_rep;
+        {
+            uint32_t qset = 0;
+            for (size_t i = 0; i < m; i++) qset |= 1u << (qv.seq[i] & 31);
+            cls_of.resize(D.alpha);
+            for (uint32_t c = 0; c < D.alpha; c++) {
+                const int64_t* rc = M + ((size_t)D.code_of[c] << 5);
+                size_t k = 0;
+                for (; k < cls_rep.size(); k++) {
+                    const int64_t* rk = M + ((size_t)cls_rep[k] << 5);
+                    bool same = true;
+                    for (int y = 0; y < 32 && same; y++) same = !((qset >> y) & 1) || rc[y] == rk[y];
+                    if (same) break;
+                }
+                if (k == cls_rep.size()) cls_rep.push_back(D.code_of[c]);
+                cls_of[c] = (uint8_t)k;
+            }
+        }
+        auto pair_wgs = [&](size_t a) {
+            const size_t b = (a + 1) * (a + 1) * (pnp_v + 4) * 4;
+            return b > kPairLdsMax ? (size_t)0 : std::min<size_t>(3, (160 * 1024) / b);
+        };
+        const bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
+                             pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
+        const uint4* dres = D.d_res;
+        if (use_cls) {
+            if (D.cls_key != cls_of) {
+                // earlier views of a pipelined search may still read the buffer
+                if (piped && v > 0) check(hipStreamSynchronize(D.stream), "sync");
+                if (!D.d_res_cls) check(hipMalloc((void**)&D.d_res_cls, D.nblocks * 1024), "class-coded residues");
+                RecodeArgs ra{};
+                ra.in = D.d_res;
+                ra.out = D.d_res_cls;
+                ra.n16 = D.nblocks * 64;
+                for (int c = 0; c < 64; c++) ra.map[c] = (uint8_t)cls_rep.size();   // padding / unused codes
+                for (uint32_t c = 0; c < D.alpha; c++) ra.map[c] = cls_of[c];
+                check(launch_recode(ra, D.stream), "recode launch");
+                D.cls_key = cls_of;
+            }
+            dres = D.d_res_cls;
+        }
+        const std::vector<uint8_t>& code_of = use_cls ? cls_rep : D.code_of;
         // profile bounds over the residue codes the DB holds
-        const uint32_t A = D.alpha;
+        const uint32_t A = (uint32_t)code_of.size();
         int64_t minM = INT64_MAX, maxM = INT64_MIN;
         for (size_t i = 0; i < m; i++)
             for (uint32_t c = 0; c < A; c++) {
-                const int64_t x = M[(D.code_of[c] << 5) + qv.seq[i]];
+                const int64_t x = M[(code_of[c] << 5) + qv.seq[i]];
                 minM = std::min(minM, x);
                 maxM = std::max(maxM, x);
             }
@@ -894,7 +946,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // (the pair kernel's tables are built on the device: pair_tables_kernel)
         std::vector<uint16_t> P(use_pair ? 0 : (size_t)(A + 1) * mpad, (uint16_t)padv);
         for (uint32_t c = 0; c < (use_pair ? 0u : A); c++) {
-            const int64_t* row = M + ((size_t)D.code_of[c] << 5);
+            const int64_t* row = M + ((size_t)code_of[c] << 5);
             uint16_t* pc = P.data() + (size_t)c * mpad;
             for (size_t i = 0; i < m; i++)
                 pc[i] = (uint16_t)(int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, row[qv.seq[i]] + rel));
@@ -936,7 +988,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // the int64 kernel scores compact codes too
         int64_t Mc[1024];
         for (int x = 0; x < 32; x++)
-            for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(D.code_of[x] << 5) + y] : -1;
+            for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(code_of[x] << 5) + y] : -1;
         const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
         // a multi-view search's earlier views may still be queued on the
         // stream: drain it before a device buffer they read is reallocated
@@ -1039,7 +1091,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
 
         StripArgs a{};
-        a.res = D.d_res;
+        a.res = dres;
         a.rowbuf = D.d_rowbuf;
         a.groups = D.d_groups;
         a.lane_len = D.d_lane_len;
@@ -1060,7 +1112,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         a.nw_base = nw_base;
 
         WideArgs w{};
-        w.res = D.d_res;
+        w.res = dres;
         w.groups = D.d_groups;
         w.lane_len = D.d_lane_len;
         w.ovf_list = ovf + 1;
@@ -1090,7 +1142,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             // pair kernel (enqueued first, so their waves start first)
             const int rl = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
             LongArgs la{};
-            la.res = D.d_res;
+            la.res = dres;
             la.groups = D.d_groups;
             la.lane_len = D.d_lane_len;
             la.lane_out = D.d_lane_out;
@@ -1148,7 +1200,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 ordinary |= (int)ok << b;
             }
             FlagArgs fa{};
-            fa.res = D.d_res;
+            fa.res = dres;
             fa.groups = D.d_groups;
             fa.lane_len = D.d_lane_len;
             fa.lane_out = D.d_lane_out;

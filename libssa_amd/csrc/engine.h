@@ -101,6 +101,10 @@ struct DeviceDB {
     // for residue code code_of[c]; code alpha is the padding column
     std::vector<uint8_t> code_of;
     uint32_t alpha = 0;
+    // per-query residue classes (device_search): class-coded copy of d_res
+    // and the class map it was made with
+    uint4* d_res_cls = nullptr;
+    std::vector<uint8_t> cls_key;
     size_t rec_begin = 0, rec_end = 0;    // plugin records [rec_begin, rec_end) of this shard
     void release();
 };

@@ -7,7 +7,7 @@ namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
 constexpr int kPairWaves = 4;      // waves per pair_kernel workgroup (they share one pair table)
-constexpr size_t kPairLdsMax = 80 * 1024;   // pair table budget (35 KiB for proteins: 4 workgroups per CU)
+constexpr size_t kPairLdsMax = 160 * 1024;  // pair table budget: one workgroup per CU (49 KiB for 20-letter proteins: 3)
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
 struct GroupDesc {
@@ -95,7 +95,7 @@ struct FilterArgs {
     const uint32_t* order;     // [n] score index of insertion position p (null: identity) -- the
                                // chunk-interleaved order of multi-view searches
     uint32_t n, k, nblocks;
-    int32_t* summary;         // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
+    int32_t* summary;          // [nblocks][kFilterMaxK] top-k mini maxima per block, descending
     int32_t* thresh;           // [nblocks] bound from earlier blocks
     int32_t* thresh_local;     // [nblocks * 64] bound from earlier minis of the same block
     int32_t* before;           // [nblocks][kFilterMaxK] scan scratch
@@ -159,6 +159,16 @@ struct CountArgs {
     unsigned long long* out;   // [2]
 };
 hipError_t launch_count(const CountArgs& a, hipStream_t st);
+
+// Residue recode (per-query residue classes, engine.cpp device_search):
+// out byte = map[in byte] over n16 16-byte words of the packed layout.
+struct RecodeArgs {
+    const uint4* in;
+    uint4* out;
+    size_t n16;
+    uint8_t map[64];
+};
+hipError_t launch_recode(const RecodeArgs& a, hipStream_t st);
 
 // pair_kernel's per-search pair tables, built on the device from the query
 // and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)

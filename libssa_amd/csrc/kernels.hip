@@ -1059,6 +1059,32 @@ hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ recode
+__global__ void __launch_bounds__(256) recode_kernel(const RecodeArgs a) {
+    __shared__ uint8_t map[64];
+    if (threadIdx.x < 64) map[threadIdx.x] = a.map[threadIdx.x];
+    __syncthreads();
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n16; i += (size_t)gridDim.x * 256) {
+        const uint4 v = a.in[i];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) o |= (uint32_t)map[(w[k] >> (8 * b)) & 63u] << (8 * b);
+            w[k] = o;
+        }
+        a.out[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+hipError_t launch_recode(const RecodeArgs& a, hipStream_t st) {
+    if (a.n16 == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<size_t>((a.n16 + 255) / 256, 8192);
+    hipLaunchKernelGGL(recode_kernel, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ long entries
 // One wave per DB entry of the longest groups, so that a handful of entries
 // far longer than the rest no longer set the launch's duration (one lane of

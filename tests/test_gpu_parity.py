@@ -1084,3 +1084,32 @@ def test_every_lane_rescored_exactly(gaps, tmp_path):
     assert [(h["score"], h["id"]) for h in S.sw_align(qq, 20, 16)] == po.search(0, q, seqs, M, gaps[0], gaps[1], 20)
     assert S.stats()["wide_count"] == len(off) - 1
     S.free_sequence(qq)
+
+
+def test_residue_classes_follow_the_query(tmp_path):
+    """28-symbol DB (the reference generator's alphabet): per-query residue
+    classes (codes whose matrix rows agree on the query's residues share one
+    code on the device) change with the query -- a standard-residue query, one
+    holding X and '*', one holding U and O -- and every full score vector and
+    top-k equals the oracle's, SW and NW, queries alternating so the cached
+    class-coded residues are rebuilt and reused."""
+    codes, off = syn.protein_db_range(20000, 5, alphabet="uniform28", lengths="uniform", lo=16, hi=600)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    base = syn.protein_query(300, 3)
+    qs = [base.copy(), base.copy(), base.copy()]
+    qs[1][::17] = syn.AA_ORDER.index("X")
+    qs[1][5::23] = syn.AA_ORDER.index("*")
+    qs[2][::19] = syn.AA_ORDER.index("U")
+    qs[2][7::29] = syn.AA_ORDER.index("O")
+    seqs = [codes[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    for q in qs + qs[::-1]:
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        for algo in (S.SW, S.NW):
+            got, _ = _full_scores(qq, algo, len(off) - 1)
+            assert (got == po.scores(algo, q, codes, off, M, -11, -1)).all(), algo
+            fn = S.sw_align if algo == S.SW else S.nw_align
+            assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.search(algo, q, seqs, M, -11, -1, 10)
+            assert S.stats()["kernel"].startswith("pair"), S.stats()["kernel"]
+        S.free_sequence(qq)
