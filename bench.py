@@ -407,7 +407,7 @@ def main():
                                  "frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None}},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
-                   "wide_ms_avg": round(float(np.mean(wide_ms)), 4),
+                   "wide_ms_avg": round(float(np.mean(wide_ms)), 4), "wide_count": int(st["wide_count"]),
                    "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,
                    "valu_issue_frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None,
                    "valu_instr_per_cell": instr_per_cell},

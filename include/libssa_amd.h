@@ -81,6 +81,11 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "no_filter" 0|1      1: copy every score back (no device top-k filter)
  *   "long_groups" -1|0|N leading groups scored one entry per wave: auto, never, N
  *   "long_share_pct" P   auto threshold: P % of one SIMD's share of all columns
+ *   "long_waves" 0|4|1   waves scoring one long entry (its query rows split over
+ *                        them): auto (4 for groups beyond "long4_share_pct", 1
+ *                        for the rest), always 4, always 1
+ *   "long4_share_pct" P  auto: 4 waves per entry for groups longer than P % of
+ *                        one SIMD's share of all columns
  * Unknown names print a warning. */
 void ssa_amd_set_option( const char * name, long value );
 

@@ -398,6 +398,8 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "pair_np")) cfg().pair_np = (int)value;
     else if (!strcmp(name, "long_groups")) cfg().long_groups = (int)value;
     else if (!strcmp(name, "long_share_pct")) cfg().long_share_pct = (int)value;
+    else if (!strcmp(name, "long_waves")) cfg().long_waves = (int)value;
+    else if (!strcmp(name, "long4_share_pct")) cfg().long4_share_pct = (int)value;
     else print_warning("unknown option %s", name);
 }
 

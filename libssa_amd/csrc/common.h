@@ -39,6 +39,8 @@ struct Config {
     int pair_np = 24;                     // pair kernel main strip: 24 (48 rows, default) or 16 (32 rows)
     int long_groups = -1;                 // leading groups scored by long_kernel: -1 auto, 0 never, N forced
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
+    int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
+    int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
 };
 Config& cfg();
 

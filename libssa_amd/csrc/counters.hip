@@ -85,8 +85,25 @@ __global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
         else f |= (uint32_t)d << b;
     }
     if (undecided) {
-        const uint32_t i = atomicAdd(a.list, 1u);
-        a.list[1 + i] = gl;        // capacity: every lane
+        // NW, ordinary penalties: which boundary chain first falls below the
+        // threshold T = I_MIN - Q - R - 1 -- the left one (H(i,-1) = Q + (i+1)R,
+        // met after ~4 i_L cells column by column) or the top one (H(-1,j) =
+        // Q + (j+1)R, met after ~j_T cells row by row); the flag is almost
+        // always decided where the first one crosses
+        bool rows = false;
+        if (a.nw && a.rlist && a.gap_extend < 0 && (a.ordinary & 2)) {
+            const int w = (a.widths & 1) ? 8 : 16;
+            const int64_t T = -(1ll << (w - 1)) - a.gap_open - a.gap_extend - 1;
+            const int64_t Rm = -(int64_t)a.gap_extend;
+            const int64_t cross = ((int64_t)a.gap_open - T) / Rm + 2;     // i_L ~ j_T
+            const int64_t n4 = (len + 3) & ~3u, full = (int64_t)a.m * n4;
+            const int64_t cost_col = a.m > cross ? 4 * cross : full;
+            const int64_t cost_row = n4 > cross && n4 <= a.rstride ? cross : full;
+            rows = cost_row * 16 < cost_col;
+        }
+        uint32_t* L = rows ? a.rlist : a.list;
+        const uint32_t i = atomicAdd(L, 1u);
+        L[1 + i] = gl;             // capacity: every lane
     } else {
         a.flags[o] = (uint8_t)f;
     }
@@ -205,6 +222,76 @@ __device__ int replay_sw(const FlagArgs& a, const LaneSeq& d, int w, int32_t* he
     return 0;
 }
 
+// search_simd_nw.c's saturated w-bit NW recurrence for one channel, the same
+// cell values as replay_nw but computed row by row (the DP is a function of
+// each cell's neighbours; the processing order is free): boundaries are the
+// reference's saturating chains -- H(-1, j-1) = 0, trunc(Q + jR) (j = 1..3),
+// then +R; F into row 0 = sat(Ft(j) + Q + R), Ft(j) = trunc(Q + (j+1)R) (j <
+// 4), then +R; H(i, -1) = QR, then +R; E into column 0 = H(i, -1) + QR.
+// Scratch per lane: H(i-1, j) and F(i, j) for the entry's n4 columns.
+__device__ int replay_nw_rows(const FlagArgs& a, const LaneSeq& d, int w, int32_t* hep, uint32_t stride) {
+    const int32_t IMIN = -(1 << (w - 1)), IMAX = (1 << (w - 1)) - 1;
+    const int64_t Q = a.gap_open, R0 = a.gap_extend;
+    const int32_t QR = trunc_w(Q + R0, w), R = trunc_w(R0, w);
+    const int32_t T = trunc_w(IMIN - Q - R0 - 1, w);
+    const uint32_t m = a.m, n4 = (d.len + 3) & ~3u;
+    int32_t hmin = 0, hmax = 0, score = 0;
+    int32_t Lprev = 0;                                   // H(i-1, -1); row 0: H(-1,-1) = 0
+    int32_t L = QR;                                      // H(i, -1)
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t qc = a.query[i];
+        int32_t diag = Lprev;                            // H(i-1, j-1) for j = 0
+        int32_t E = sat_w(L + QR, IMIN, IMAX);           // E into column 0
+        int32_t top = 0, Ft = 0;                         // row 0: H(-1, j-1) chain and Ft chain
+        for (uint32_t j = 0; j < n4; j++) {
+            int32_t Fin, up;
+            if (i == 0) {
+                // H(-1, j) (the next column's diagonal) and F into row 0
+                Ft = j < 4 ? trunc_w(Q + (int64_t)(j + 1) * R0, w) : sat_w(Ft + R, IMIN, IMAX);
+                Fin = sat_w(Ft + QR, IMIN, IMAX);
+                const uint32_t jn = j + 1;
+                top = jn < 4 ? trunc_w(Q + (int64_t)jn * R0, w) : sat_w(top + R, IMIN, IMAX);
+                up = top;
+            } else {
+                Fin = hep[(size_t)(2 * j + 1) * stride];
+                up = hep[(size_t)(2 * j) * stride];
+            }
+            int32_t H = sat_w(diag + trunc_w(d.row(a, j)[qc], w), IMIN, IMAX);
+            H = max(H, Fin);
+            H = max(H, E);
+            hmin = min(hmin, H);
+            hmax = max(hmax, H);
+            if (i + 1 == m && j + 1 == d.len) score = H;
+            const int32_t t = sat_w(H + QR, IMIN, IMAX);
+            hep[(size_t)(2 * j + 1) * stride] = max(sat_w(Fin + R, IMIN, IMAX), t);
+            hep[(size_t)(2 * j) * stride] = H;
+            E = max(sat_w(E + R, IMIN, IMAX), t);
+            diag = up;
+        }
+        if (hmin < T || hmax == IMAX) return 1;
+        Lprev = L;
+        L = sat_w(L + R, IMIN, IMAX);
+    }
+    return score <= IMIN || score >= IMAX;
+}
+
+__global__ void __launch_bounds__(64) flags_replay_rows_kernel(const FlagArgs a) {
+    const uint32_t n = *a.rlist;
+    const uint32_t tid = blockIdx.x * 64 + threadIdx.x;
+    int32_t* hep = a.rwork + tid;
+    for (uint32_t i = tid; i < n; i += a.rthreads) {
+        const uint32_t gl = a.rlist[1 + i];
+        const uint32_t g = gl >> 6, lane = gl & 63;
+        LaneSeq d{(const uint8_t*)a.res + (size_t)a.groups[g].blk * 1024 + lane * 16, a.lane_len[gl]};
+        uint32_t f = 0;
+        for (int b = 0; b < 2; b++) {
+            if (!((a.widths >> b) & 1)) continue;
+            f |= (uint32_t)replay_nw_rows(a, d, b ? 16 : 8, hep, a.rthreads) << b;
+        }
+        a.flags[a.lane_out[gl]] = (uint8_t)f;
+    }
+}
+
 __global__ void __launch_bounds__(64) flags_replay_kernel(const FlagArgs a) {
     const uint32_t n = *a.list;
     const uint32_t tid = blockIdx.x * 64 + threadIdx.x;
@@ -257,8 +344,10 @@ hipError_t launch_flags(const FlagArgs& a, hipStream_t st) {
     if (a.nlanes == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.list, 0, 4, st);
     if (e != hipSuccess) return e;
+    if (a.rlist && (e = hipMemsetAsync(a.rlist, 0, 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(flags_decide_kernel, dim3((a.nlanes + 255) / 256), dim3(256), 0, st, a);
     if (a.m > 0) hipLaunchKernelGGL(flags_replay_kernel, dim3(a.threads / 64), dim3(64), 0, st, a);
+    if (a.m > 0 && a.rlist) hipLaunchKernelGGL(flags_replay_rows_kernel, dim3(a.rthreads / 64), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

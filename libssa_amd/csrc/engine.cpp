@@ -45,7 +45,8 @@ void DeviceDB::release() {
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch);
-    dfree(d_flags); dfree(d_flist); dfree(d_cnt); dfree(d_res_cls);
+    dfree(d_flags); dfree(d_flist); dfree(d_cnt); dfree(d_res_cls); dfree(d_frlist); dfree(d_frwork);
+    d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
     d_res_cls = nullptr;
     cls_key.clear();
     if (h_cnt) (void)hipHostFree(h_cnt);
@@ -326,6 +327,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     if (!D.stream) {
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
         check(hipStreamCreateWithFlags(&D.stream_long, hipStreamNonBlocking), "hipStreamCreate");
+        check(hipStreamCreateWithFlags(&D.stream_long1, hipStreamNonBlocking), "hipStreamCreate");
         for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -360,6 +362,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     dalloc((void**)&D.d_wide, std::max<size_t>(H.lane_len.size(), 1) * 8, "wide scores");
     D.ovf_slices = 1;
     dalloc((void**)&D.d_flist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
+    dalloc((void**)&D.d_frlist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
     dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe, "overflow counters");
     check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe, hipHostMallocDefault), "pinned");
     D.upblk_cap = kUpHeader + 16384 + 4096;
@@ -922,7 +925,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 const size_t beyond = (size_t)(D.len_sorted.end() -
                                                std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
                 const uint32_t lg = long_plan(D, m, beyond, Q, R, minM, maxM);
-                if (lg != UINT32_MAX || beyond <= 64) {
+                // (an entry beyond the bound would also corrupt its group's
+                // other lanes, whose padding columns run to its length: the
+                // group must go to long_kernel, or the strip kernels run)
+                if (lg != UINT32_MAX) {
                     use_pair = true;
                     nmax16 = lim;
                     long_groups = lg == UINT32_MAX ? 0 : lg;
@@ -1071,25 +1077,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // search its own slice (all views stay on the device until the end)
         uint32_t* ovf = D.d_ovf + (piped ? v * (ovf_capv + 1) : 0);
         int64_t* wide = D.d_wide + (piped ? v * ovf_capv : 0);
-        if (use_pair) {
-            TableArgs ta{};
-            ta.query = D.d_query;
-            ta.matrix = D.d_matrix;
-            ta.out = D.d_qpt;
-            ta.m = (uint32_t)m;
-            ta.alpha = A;
-            ta.np = (uint32_t)pnp;
-            ta.nmain = main_strips;
-            ta.npt = (uint32_t)tail_np;
-            ta.tail_row0 = main_strips * 2 * (uint32_t)pnp;
-            ta.rel = rel;
-            ta.pad = (uint32_t)(uint16_t)padv;
-            ta.zero = ovf;
-            check(launch_pair_tables(ta, st), "pair tables kernel");
-        } else {
-            check(hipMemsetAsync(ovf, 0, 4, st), "memset");
-        }
-
         StripArgs a{};
         a.res = dres;
         a.rowbuf = D.d_rowbuf;
@@ -1137,10 +1124,20 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (v == 0) prep = now_ms() - t_prep0;
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         check(hipEventRecord(ev_k0, st), "event");
+        uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         if (long_groups > 0) {
-            // the longest groups on the second stream, concurrently with the
-            // pair kernel (enqueued first, so their waves start first)
-            const int rl = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
+            // the longest groups on their own streams, concurrently with the
+            // pair kernel (enqueued first, so their waves start first): one
+            // wave per entry (RL rows per lane, 64*RL rows per pass), or --
+            // for the groups so long that one wave's latency would outlast
+            // the pair kernel -- one workgroup per entry, its rows over 4
+            // waves (RL 2 up to 512 rows, else 4, passes of 1024 rows)
+            if (C.long_waves == 4) {
+                long4 = long_groups;
+            } else if (C.long_waves == 0) {
+                const double thr4 = (double)D.ncols_sum / D.nsimd * C.long4_share_pct / 100.0;
+                while (long4 < long_groups && D.group_ncols[long4] > thr4) long4++;
+            }
             LongArgs la{};
             la.res = dres;
             la.groups = D.d_groups;
@@ -1149,26 +1146,61 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             la.query = D.d_query;
             la.matrix = D.d_matrix;
             la.scores = a.scores;
-            la.nseq = long_groups * 64;
             la.m = (uint32_t)m;
             la.alpha = A;
             la.gap_open = Q;
             la.gap_extend = R;
-            if (m > (size_t)64 * rl) {
+            const int rl4 = m <= 512 ? 2 : 4;
+            const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
+            if (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1) {
                 la.stride = D.group_ncols[0] + 16;
-                const size_t need = (size_t)la.nseq * la.stride;
+                const size_t need = (size_t)long_groups * 64 * la.stride;
                 if (D.lscratch_cap < need) {
                     check(hipStreamSynchronize(D.stream_long), "sync");
+                    check(hipStreamSynchronize(D.stream_long1), "sync");
                     dfree(D.d_lscratch);
                     check(hipMalloc((void**)&D.d_lscratch, need * 8), "long-entry scratch");
                     D.lscratch_cap = need;
                 }
                 la.scratch = D.d_lscratch;
             }
-            check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
-            check(launch_long(la, rl, nw, D.stream_long), "long kernel launch");
-            check(hipEventRecord(D.ev[7], D.stream_long), "event");
+            if (long4 > 0) {
+                la.seq0 = 0;
+                la.nseq = long4 * 64;
+                check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
+                check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
+                check(hipEventRecord(D.ev[7], D.stream_long), "event");
+            }
+            if (long4 < long_groups) {
+                la.seq0 = long4 * 64;
+                la.nseq = (long_groups - long4) * 64;
+                check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
+                check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
+                check(hipEventRecord(D.ev[6], D.stream_long1), "event");
+            }
         }
+        // the pair tables after the long entries' launch: long_kernel only
+        // needs the uploads, so its workgroups are dispatched before the
+        // pair kernel's fill the CUs' LDS (they are the critical path)
+        if (use_pair) {
+            TableArgs ta{};
+            ta.query = D.d_query;
+            ta.matrix = D.d_matrix;
+            ta.out = D.d_qpt;
+            ta.m = (uint32_t)m;
+            ta.alpha = A;
+            ta.np = (uint32_t)pnp;
+            ta.nmain = main_strips;
+            ta.npt = (uint32_t)tail_np;
+            ta.tail_row0 = main_strips * 2 * (uint32_t)pnp;
+            ta.rel = rel;
+            ta.pad = (uint32_t)(uint16_t)padv;
+            ta.zero = ovf;
+            check(launch_pair_tables(ta, st), "pair tables kernel");
+        } else {
+            check(hipMemsetAsync(ovf, 0, 4, st), "memset");
+        }
+
         if (use_pair) {
             StripArgs b = a;
             b.nstrips = main_strips;
@@ -1180,7 +1212,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
-        if (long_groups > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
+        if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
+        if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
         check(hipEventRecord(ev_k1, st), "event");
         check(launch_wide(w, wide_threads, st), "wide kernel launch");
         if (want_counts) {
@@ -1221,6 +1254,21 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             fa.ordinary = ordinary;
             fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
             fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
+            if (nw && D.ngroups > 0) {
+                // row-major NW replay: scratch for the longest entry's
+                // columns, 64..1024 lanes within 64 MiB
+                fa.rstride = D.group_ncols[0];
+                fa.rthreads = (uint32_t)std::max<size_t>(64, std::min<size_t>(1024, (64ull << 20) / (8ull * fa.rstride)) / 64 * 64);
+                const size_t need = (size_t)fa.rthreads * 2 * fa.rstride;
+                if (D.frwork_cap < need) {
+                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                    dfree(D.d_frwork);
+                    check(hipMalloc((void**)&D.d_frwork, need * 4), "row-major replay scratch");
+                    D.frwork_cap = need;
+                }
+                fa.rlist = D.d_frlist;
+                fa.rwork = D.d_frwork;
+            }
             check(launch_flags(fa, st), "overflow flags launch");
             if (ind || v + 1 == V) {
                 // a batch query's own counters, or the search's over all views

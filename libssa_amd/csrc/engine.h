@@ -84,6 +84,9 @@ struct DeviceDB {
     uint8_t* d_flags = nullptr;
     size_t flags_cap = 0;
     uint32_t* d_flist = nullptr;          // [0] count, then up to ngroups * 64 lanes
+    uint32_t* d_frlist = nullptr;         // the same for the row-major NW replay
+    int32_t* d_frwork = nullptr;          // its scratch
+    size_t frwork_cap = 0;                // int32 elements
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
     unsigned long long* h_cnt = nullptr;  // pinned mirror
     // long entries (long_kernel, launched on stream_long beside the pair
@@ -92,7 +95,8 @@ struct DeviceDB {
     std::vector<uint32_t> group_ncols;
     uint64_t ncols_sum = 0;
     uint32_t nsimd = 1024;
-    hipStream_t stream_long = nullptr;
+    hipStream_t stream_long = nullptr;    // long_kernel, 4 waves per entry (event ev[7])
+    hipStream_t stream_long1 = nullptr;   // long_kernel, 1 wave per entry (event ev[6])
     int64_t* d_lscratch = nullptr;
     size_t lscratch_cap = 0;              // int64 elements
     std::vector<uint32_t> lane_out;       // host copy for overflow mapping

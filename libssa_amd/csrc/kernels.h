@@ -42,10 +42,10 @@ struct StripArgs {
     uint32_t g_first;
 };
 
-// Long DB entries (long_kernel): one wave per entry, the query rows split over
-// the 64 lanes (RL consecutive rows per lane, passes of 64*RL rows), DB
-// columns swept as a lane-skewed wavefront; exact int32 arithmetic.  Serves
-// the entries of the first nseq/64 (longest) groups, which pair_kernel then
+// Long DB entries (long_kernel): the query rows split over the lanes of W
+// waves (RL consecutive rows per lane, passes of W*64*RL rows), DB columns
+// swept as a lane-skewed wavefront; exact int32 arithmetic.  Serves the
+// entries of the first nseq/64 (longest) groups, which pair_kernel then
 // skips (StripArgs::g_first).
 struct LongArgs {
     const uint4* res;
@@ -57,7 +57,7 @@ struct LongArgs {
     int32_t* scores;
     int64_t* scratch;          // [nseq][stride] (H, F) of a pass's last row (multi-pass only)
     uint32_t stride;
-    uint32_t nseq;             // entries served: lanes [0, nseq) of the group order
+    uint32_t seq0, nseq;       // entries served: lanes [seq0, seq0 + nseq) of the group order
     uint32_t m, alpha;
     int32_t gap_open, gap_extend;
 };
@@ -115,8 +115,11 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st);
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 // rl: rows per lane (4, 8, 12 or 16; 64*rl rows per pass)
-hipError_t launch_long(const LongArgs& a, int rl, bool nw, hipStream_t st);
-size_t long_lds_bytes(uint32_t alpha, int rl);
+// w: waves per entry (1: four entries per workgroup; 4: one entry, its
+// rows over the workgroup's waves); rl: rows per lane (w 1: 4, 8, 12 or 16;
+// w 4: 2 or 4); w * 64 * rl rows per pass
+hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st);
+size_t long_lds_bytes(uint32_t alpha, int w, int rl);
 
 // The reference's 8/16-bit overflow counters (counters.hip).  m_run reports
 // how many (query view, DB sequence) pairs its w-bit SIMD kernels sent on to
@@ -137,9 +140,15 @@ struct FlagArgs {
     const int64_t* matrix;     // [1024] compact code x query code
     const int64_t* padrow;     // [32] M[0][y]: the reference pads a sequence to 4 columns with code 0
     uint8_t* flags;            // this view's [entries]
-    uint32_t* list;            // [0] count, [1..nlanes] lanes left to the replay
+    uint32_t* list;            // [0] count, [1..nlanes] lanes left to the replay (column-major)
     int32_t* work;             // replay scratch, [2m][threads] (thread-interleaved)
     uint32_t nlanes, m, threads;
+    // NW lanes whose top boundary crosses the flag threshold within the
+    // entry (entries of ~16 k+ residues at 16 bits): row-major replay, which
+    // meets the flagging cell within the first row instead of m x that
+    uint32_t* rlist;           // [0] count, [1..nlanes] lanes
+    int32_t* rwork;            // [2 rstride][rthreads]
+    uint32_t rstride, rthreads;
     int32_t gap_open, gap_extend;
     int32_t nw;
     int32_t widths;            // bit 0: 8-bit flags wanted, bit 1: 16-bit

@@ -1085,170 +1085,6 @@ hipError_t launch_recode(const RecodeArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------ long entries
-// One wave per DB entry of the longest groups, so that a handful of entries
-// far longer than the rest no longer set the launch's duration (one lane of
-// pair_kernel scores a whole entry: its wave runs ncols x strips steps while
-// the rest of the chip has drained).  The query's rows are split over the
-// lanes -- lane l holds rows i0p + l*RL .. + RL-1 of pass p (64*RL rows per
-// pass) -- and the entry's columns sweep through the lanes as a skewed
-// wavefront: at step t lane l scores column j = t - l of its rows, taking H
-// and F of the row above (lane l-1's last row at column j, made at step t-1)
-// and the residue through a one-lane DPP shift.  The recurrences are the
-// reference's 64-bit scorers (smith_waterman_63.c:32-98,
-// needleman_wunsch_64.c:32-98; oracle_full_sw / oracle_full_nw), in int32,
-// exact under the host's bound (engine.cpp).  A pass's last row is kept in
-// scratch for the next pass's lane 0.
-__device__ __forceinline__ int32_t shr1(int32_t lane0_value, int32_t v) {
-    // DPP wave_shr:1 -- lane l receives lane l-1's v, lane 0 keeps lane0_value
-    return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138, 0xf, 0xf, false);
-}
-
-template <int RL, bool NW>
-__global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int16_t ltab[];
-    constexpr uint32_t RP = 64 * RL;
-    // these waves are the launch's critical path: they issue before the
-    // pair kernel's waves sharing their SIMD
-    __builtin_amdgcn_s_setprio(3);
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t s = blockIdx.x * kLongWaves + wave;
-    const bool active = s < a.nseq;
-    const uint32_t ss = active ? s : 0;
-    const GroupDesc gd = a.groups[ss >> 6];
-    const uint32_t n = a.lane_len[ss];
-    const uint4* rp = a.res + (size_t)gd.blk * 64 + (ss & 63);
-    int64_t* scr = a.scratch + (size_t)ss * a.stride;
-    const int32_t Q = a.gap_open, R = a.gap_extend, QR = Q + R;
-    const uint32_t m = a.m, prow = a.alpha + 1;
-    const uint32_t npass = (m + RP - 1) / RP;
-    int32_t S = 0, score = 0;
-    for (uint32_t p = 0; p < npass; p++) {
-        const uint32_t i0p = p * RP;
-        // the pass's profile [code][row] (padding code and rows: -4096); the
-        // fence orders the previous pass's scratch stores before its loads
-        __threadfence();
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < prow * RP; t += 64 * kLongWaves) {
-            const uint32_t c = t / RP, i = i0p + t % RP;
-            ltab[t] = (c < a.alpha && i < m) ? (int16_t)a.matrix[(c << 5) + a.query[i]] : (int16_t)-4096;
-        }
-        __syncthreads();
-        if (!active || n == 0) continue;
-        const bool lastp = p + 1 == npass;
-        const int i0 = (int)(i0p + lane * RL);
-        const int lmax = (int)((min(m - i0p, RP) - 1) / RL);   // last lane holding query rows
-        // left boundary: H(i, -1) and E into column 0
-        int32_t H[RL], E[RL];
-#pragma unroll
-        for (int r = 0; r < RL; r++) {
-            H[r] = NW ? Q + (i0 + r + 1) * R : 0;
-            E[r] = NW ? 2 * Q + (i0 + r + 2) * R : 0;
-        }
-        int32_t hdiag = NW ? (i0 == 0 ? 0 : Q + i0 * R) : 0;   // H(i0-1, -1)
-        int32_t hbot = 0, fbot = 0;
-        uint32_t d = 0;
-        // residues and (later passes) the previous pass's last row are
-        // fetched a 16-column block ahead; the row is lane-distributed (lane
-        // k holds column 16b + (k & 15)) and read back with v_readlane
-        uint4 blk = rp[0], blk_next = n > 16 ? rp[64] : make_uint4(0, 0, 0, 0);
-        auto scr_load = [&](uint32_t c) -> int64_t {
-            return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        };
-        int64_t row = 0, row_next = 0;
-        if (p > 0) {
-            row = scr_load(lane & 15);
-            row_next = scr_load(16 + (lane & 15));
-        }
-        const uint32_t steps = n + (uint32_t)lmax;
-        for (uint32_t t = 0; t < steps; t++) {
-            // lane 0's inputs at column t: the top boundary H(-1, t), F into
-            // row 0 (first pass), or the previous pass's last row
-            int32_t th = 0, tf = 0;
-            uint32_t dn = 0;
-            if (t < n) {
-                if ((t & 15) == 0 && t > 0) {
-                    blk = blk_next;
-                    if (t + 16 < n) blk_next = rp[(size_t)((t >> 4) + 1) * 64];
-                    if (p > 0) {
-                        row = row_next;
-                        row_next = scr_load(t + 16 + (lane & 15));
-                    }
-                }
-                if (p == 0) {
-                    if (NW) {
-                        th = Q + ((int32_t)t + 1) * R;
-                        tf = 2 * Q + ((int32_t)t + 2) * R;
-                    }
-                } else {
-                    th = __builtin_amdgcn_readlane((int32_t)row, t & 15);
-                    tf = __builtin_amdgcn_readlane((int32_t)(row >> 32), t & 15);
-                }
-                const uint32_t w = (t & 8) ? ((t & 4) ? blk.w : blk.z) : ((t & 4) ? blk.y : blk.x);
-                dn = (w >> (8 * (t & 3))) & 0xffu;
-            }
-            const int32_t hin = shr1(th, hbot);
-            const int32_t fin = shr1(tf, fbot);
-            d = (uint32_t)shr1((int32_t)dn, (int32_t)d);
-            const int j = (int)t - lane;
-            if (lane <= lmax && j >= 0 && j < (int)n) {
-                const uint2* pp = (const uint2*)(ltab + d * RP + lane * RL);
-                int32_t P[RL];
-#pragma unroll
-                for (int q = 0; q < RL / 4; q++) {
-                    const uint2 v = pp[q];
-                    P[4 * q] = (int32_t)(int16_t)(v.x & 0xffffu);
-                    P[4 * q + 1] = (int32_t)v.x >> 16;
-                    P[4 * q + 2] = (int32_t)(int16_t)(v.y & 0xffffu);
-                    P[4 * q + 3] = (int32_t)v.y >> 16;
-                }
-                int32_t hd = hdiag, f = fin;
-#pragma unroll
-                for (int r = 0; r < RL; r++) {
-                    const int32_t up = H[r];
-                    // SW keeps E and F clamped at 0, which makes h >= 0 with
-                    // no extra max: exact for R <= 0 (max(E,0) + R <= 0
-                    // wherever E < 0, so every max(., 0) downstream agrees)
-                    const int32_t h = max(max(hd + P[r], E[r]), f);
-                    if (!NW) S = max(S, h);
-                    H[r] = h;
-                    const int32_t tt = h + QR;
-                    E[r] = NW ? max(E[r] + R, tt) : max(max(E[r] + R, tt), 0);
-                    f = NW ? max(f + R, tt) : max(max(f + R, tt), 0);
-                    hd = up;
-                }
-                hdiag = hin;
-                hbot = H[RL - 1];
-                fbot = f;
-                if (!lastp && lane == 63)
-                    __hip_atomic_store(scr + j, (int64_t)(uint32_t)hbot | ((int64_t)fbot << 32), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (NW && lastp) {
-            // H(m-1, n-1): the lane holding row m-1 stopped updating after
-            // column n-1
-            const uint32_t rr = m - 1 - i0p;
-            int32_t hs = H[0];
-#pragma unroll
-            for (int r = 1; r < RL; r++) hs = (rr % RL == (uint32_t)r) ? H[r] : hs;
-            score = __builtin_amdgcn_readlane(hs, rr / RL);
-        }
-    }
-    if (!active) return;
-    const uint32_t o = a.lane_out[ss];
-    if (o == 0xffffffffu) return;
-    if (!NW) {
-        for (int x = 32; x > 0; x >>= 1) S = max(S, __shfl_xor(S, x));
-        score = S;
-    }
-    if (n == 0) score = NW ? Q + (int32_t)m * R : 0;
-    if (lane == 0) a.scores[o] = score;
-}
-
-size_t long_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * rl * 2; }
-
 // hipFuncSetAttribute (dynamic LDS above 64 KiB) once per kernel and device:
 // the per-device search threads of a multi-GPU search launch concurrently
 static hipError_t lds_attr_once(const void* fn, std::atomic<uint64_t>& done, int bytes) {
@@ -1262,24 +1098,362 @@ static hipError_t lds_attr_once(const void* fn, std::atomic<uint64_t>& done, int
     return e;
 }
 
-template <int RL, bool NW>
+// ------------------------------------------------------------ long entries
+// The longest DB entries, so that a handful of entries far longer than the
+// rest no longer set the launch's duration (one lane of pair_kernel scores a
+// whole entry: its wave runs ncols x strips steps while the rest of the chip
+// has drained).  An entry's query rows are split over W waves of a workgroup
+// and their lanes -- wave w, lane l holds rows i0p + (w*64 + l)*RL .. + RL-1
+// of pass p (W*64*RL rows per pass) -- and its columns sweep through them as
+// a skewed wavefront: at step t lane l of a wave scores column j = t - l of
+// its rows, taking H and F of the row above (lane l-1's last row at column j,
+// made at step t-1) and the residue through a one-lane DPP shift.  Lane 0 of
+// wave w > 0 takes them from wave w-1's lane 63 through an LDS ring (one
+// (H, F) pair per column); lane 0 of wave 0 from the top boundary (first
+// pass) or from the previous pass's last row, which the last wave left in
+// scratch.  The waves advance in supersteps of 64 steps separated by a
+// workgroup barrier, wave w running 2 supersteps behind wave w-1: a column's
+// ring entry is always written a superstep before it is read, and read
+// before the ring wraps (kLongRing columns).  W = 4 cuts an entry's latency
+// by ~4x against one wave (W = 1: four entries per workgroup, one wave each,
+// sharing the pass's profile table).  The recurrences are the reference's
+// 64-bit scorers (smith_waterman_63.c:32-98, needleman_wunsch_64.c:32-98;
+// oracle_full_sw / oracle_full_nw), in int32, exact under the host's bound
+// (engine.cpp long_plan).
+constexpr uint32_t kLongRing = 256;
+
+__device__ __forceinline__ int32_t shr1(int32_t lane0_value, int32_t v) {
+    // DPP wave_shr:1 -- lane l receives lane l-1's v, lane 0 keeps lane0_value
+    return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138, 0xf, 0xf, false);
+}
+
+// one lane's profile slice: RL int16 values (rows i0 .. i0+RL-1 of a code)
+template <int RL>
+struct ProfSlice {
+    uint32_t v[RL / 2];
+};
+
+template <int W, int RL, bool NW>
+__global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][RP] profile of the pass
+    __shared__ int2 ring[W > 1 ? W - 1 : 1][W > 1 ? kLongRing : 1];
+    __shared__ int32_t wmax[kLongWaves];
+    constexpr int EPW = kLongWaves / W;              // entries per workgroup
+    constexpr uint32_t RW = 64 * RL;                 // rows per wave
+    constexpr uint32_t RP = W * RW;                  // rows per pass
+    constexpr int PF = 2;                            // profile loads issued PF steps ahead
+    // these waves are the launch's critical path: they issue before the
+    // pair kernel's waves sharing their SIMD
+    __builtin_amdgcn_s_setprio(3);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wr = wave % W;                    // rank of the wave inside its entry
+    const uint32_t s = blockIdx.x * EPW + wave / W;  // entry: lane seq0 + s of the group order
+    const bool active = s < a.nseq;
+    const uint32_t ss = a.seq0 + (active ? s : 0);
+    const GroupDesc gd = a.groups[ss >> 6];
+    const uint32_t n = active ? a.lane_len[ss] : 0;
+    const uint4* rp = a.res + (size_t)gd.blk * 64 + (ss & 63);
+    int64_t* scr = a.scratch + (size_t)ss * a.stride;
+    const int32_t Q = a.gap_open, R = a.gap_extend, QR = Q + R;
+    const uint32_t m = a.m, prow = a.alpha + 1;
+    const uint32_t npass = (m + RP - 1) / RP;
+    // supersteps: every wave of the workgroup loops over the same count
+    uint32_t nmax = n;
+    if (EPW > 1) {
+        __shared__ uint32_t nsh[kLongWaves];
+        if (lane == 0) nsh[wave] = n;
+        __syncthreads();
+        for (int e = 0; e < kLongWaves; e++) nmax = max(nmax, nsh[e]);
+    }
+    const uint32_t nsuper = (nmax + 63 + 63) / 64 + 2 * (W - 1);
+    int32_t S = 0, score = 0;
+    for (uint32_t p = 0; p < npass; p++) {
+        const uint32_t i0p = p * RP;
+        // the pass's profile [code][row] (padding code and rows: -4096); the
+        // fence orders the previous pass's scratch stores before its loads
+        __threadfence();
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < prow * RP; x += 64 * kLongWaves) {
+            const uint32_t c = x / RP, i = i0p + x % RP;
+            ltab[x] = (c < a.alpha && i < m) ? (int16_t)a.matrix[(c << 5) + a.query[i]] : (int16_t)-4096;
+        }
+        __syncthreads();
+        if (nmax == 0) continue;
+        const bool lastp = p + 1 == npass;
+        const uint32_t i0w = i0p + wr * RW;            // first row of this wave
+        const bool wact = active && n > 0 && i0w < m;
+        const int i0 = (int)(i0w + lane * RL);
+        // last lane holding query rows (a partial wave only ends the query:
+        // every wave feeding another wave or pass is full)
+        const int lmax = wact ? (int)((min(m - i0w, RW) - 1) / RL) : -1;
+        const bool feeds_ring = W > 1 && wr + 1 < W && i0w + RW < m;
+        const bool feeds_scratch = !lastp && wr + 1 == W;
+        const int16_t* prof = ltab + (i0 - i0p);          // + code * RP
+        // left boundary: H(i, -1) and E into column 0
+        int32_t H[RL], E[RL];
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            H[r] = NW ? Q + (i0 + r + 1) * R : 0;
+            E[r] = NW ? 2 * Q + (i0 + r + 2) * R : 0;
+        }
+        int32_t hdiag = NW ? (i0 == 0 ? 0 : Q + i0 * R) : 0;   // H(i0-1, -1)
+        int32_t hbot = 0, fbot = 0;
+        // residues run PF columns ahead of the DP: at step t lane l receives
+        // column t + PF - l through the DPP chain and issues the LDS load of
+        // its profile slice, consumed at step t + PF (the load's latency off
+        // the step's dependency chain).  Residues and (wave 0 of a
+        // later pass) the previous pass's last row are fetched a 16-column
+        // block ahead; the row is lane-distributed (lane k holds column
+        // 16b + (k & 15)) and read back with v_readlane
+        // (the block is kept in four scalars: as one uint4 captured by the
+        // lambda below the compiler placed it in scratch memory and read the
+        // selected dword back with a scratch load every step)
+        uint32_t d = 0;
+        uint32_t b0, b1, b2, b3, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        {
+            const uint4 v = rp[0];
+            b0 = v.x; b1 = v.y; b2 = v.z; b3 = v.w;
+            if (n > 16) {
+                const uint4 x = rp[64];
+                c0 = x.x; c1 = x.y; c2 = x.z; c3 = x.w;
+            }
+        }
+        // the next column's residue into the DPP chain, and the LDS load of
+        // this lane's profile slice for it (RL int16 = RL / 2 dwords)
+#define LONG_ISSUE(u, dst)                                                                          \
+        {                                                                                          \
+            const uint32_t u_ = (u);                                                               \
+            uint32_t dn_ = 0;                                                                      \
+            if (u_ < n) {                                                                          \
+                if ((u_ & 15) == 0 && u_ > 0) {                                                    \
+                    b0 = c0; b1 = c1; b2 = c2; b3 = c3;                                            \
+                    if (u_ + 16 < n) {                                                             \
+                        const uint4 x_ = rp[(size_t)((u_ >> 4) + 1) * 64];                         \
+                        c0 = x_.x; c1 = x_.y; c2 = x_.z; c3 = x_.w;                                \
+                    }                                                                              \
+                }                                                                                  \
+                const uint32_t w_ = (u_ & 8) ? ((u_ & 4) ? b3 : b2) : ((u_ & 4) ? b1 : b0);        \
+                dn_ = (w_ >> (8 * (u_ & 3))) & 0xffu;                                              \
+            }                                                                                      \
+            d = (uint32_t)shr1((int32_t)dn_, (int32_t)d);                                          \
+            dst = *(const ProfSlice<RL>*)(prof + d * RP);                                          \
+        }
+        auto scr_load = [&](uint32_t c) __attribute__((always_inline)) -> int64_t {
+            return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        };
+        const bool from_scr = p > 0 && wr == 0;
+        int64_t row = 0, row_next = 0;
+        ProfSlice<RL> pq0{}, pq1{};                      // slices for steps t, t+1
+        if (wact) {
+            if (from_scr) {
+                row = scr_load(lane & 15);
+                row_next = scr_load(16 + (lane & 15));
+            }
+            LONG_ISSUE(0u, pq0);
+            LONG_ISSUE(1u, pq1);
+        }
+        // wave w > 0: (H, F) of wave w-1's last row, one column ahead
+        int2 rnext = make_int2(0, 0);
+        const uint32_t steps = wact ? n + (uint32_t)lmax : 0;
+        uint32_t t = 0;
+        // the DP of one step for lanes whose column is real: RL rows, then
+        // lane 63's last row to the next wave (ring) or pass (scratch)
+#define LONG_ROWS(pcv, hin, fin, tval)                                                            \
+        {                                                                                          \
+            int32_t P_[RL];                                                                        \
+            _Pragma("unroll") for (int k_ = 0; k_ < RL / 2; k_++) {                                \
+                P_[2 * k_] = (int32_t)(int16_t)((pcv).v[k_] & 0xffffu);                            \
+                P_[2 * k_ + 1] = (int32_t)(pcv).v[k_] >> 16;                                       \
+            }                                                                                      \
+            int32_t hd_ = hdiag, f_ = (fin);                                                       \
+            _Pragma("unroll") for (int r_ = 0; r_ < RL; r_++) {                                    \
+                const int32_t up_ = H[r_];                                                         \
+                const int32_t h_ = max(max(hd_ + P_[r_], E[r_]), f_);                              \
+                if (!NW) S = max(S, h_);                                                           \
+                H[r_] = h_;                                                                        \
+                const int32_t tt_ = h_ + QR;                                                       \
+                E[r_] = NW ? max(E[r_] + R, tt_) : max(max(E[r_] + R, tt_), 0);                    \
+                f_ = NW ? max(f_ + R, tt_) : max(max(f_ + R, tt_), 0);                             \
+                hd_ = up_;                                                                         \
+            }                                                                                      \
+            /* one step at a time (unrolled, the compiler defers the max chain and hoists work) */ \
+            if (!NW) asm volatile("" : "+v"(S));                                                   \
+            asm volatile("" : "+v"(f_));                                                           \
+            hdiag = (hin);                                                                         \
+            hbot = H[RL - 1];                                                                      \
+            fbot = f_;                                                                             \
+            if ((feeds_ring || feeds_scratch) && lane == 63) {                                     \
+                const int jj_ = (int)(tval) - 63;                                                  \
+                if (feeds_ring) ring[wr][jj_ & (kLongRing - 1)] = make_int2(hbot, fbot);           \
+                if (feeds_scratch)                                                                 \
+                    __hip_atomic_store(scr + jj_, (int64_t)(uint32_t)hbot | ((int64_t)fbot << 32), \
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                \
+            }                                                                                      \
+        }
+        // 16 steps from t (t % 16 == 0, t >= 64, t + 32 <= n): every lane's
+        // column is real, every top input exists, the residue dwords and
+        // row-buffer reads are static -- no per-step masks or mode tests (the
+        // general path below runs ~4x the overhead per step).  Lanes past
+        // lmax (a partial last wave) compute rows past the query here: their
+        // profile is -4096, nothing real depends on them, and their values
+        // never exceed the real rows' (F and E only carry real values down
+        // and right with non-positive increments), so SW's maximum holds.
+        // MODE: 0 top boundary, 1 scratch row, 2 ring.
+#define LONG_STEADY(MODE)                                                                         \
+        {                                                                                          \
+            _Pragma("unroll") for (int k = 0; k < 16; k++) {                                       \
+                const uint32_t tk = t + k;                                                         \
+                const ProfSlice<RL> pcv = pq0;                                                     \
+                pq0 = pq1;                                                                         \
+                int32_t th = 0, tf = 0;                                                            \
+                if (MODE == 2) {                                                                   \
+                    th = rnext.x;                                                                  \
+                    tf = rnext.y;                                                                  \
+                    rnext = ring[wr - 1][(tk + 1) & (kLongRing - 1)];                              \
+                } else if (MODE == 1) {                                                            \
+                    if (k == 0) {                                                                  \
+                        row = row_next;                                                            \
+                        row_next = scr_load(tk + 16 + (lane & 15));                                \
+                    }                                                                              \
+                    th = __builtin_amdgcn_readlane((int32_t)row, k);                               \
+                    tf = __builtin_amdgcn_readlane((int32_t)(row >> 32), k);                       \
+                } else if (NW) {                                                                   \
+                    th = Q + ((int32_t)tk + 1) * R;                                                \
+                    tf = 2 * Q + ((int32_t)tk + 2) * R;                                            \
+                }                                                                                  \
+                if (k == 14) {                                                                     \
+                    b0 = c0; b1 = c1; b2 = c2; b3 = c3;                                            \
+                    if (tk + 18 < n) {                                                             \
+                        const uint4 x_ = rp[(size_t)(((tk + 2) >> 4) + 1) * 64];                   \
+                        c0 = x_.x; c1 = x_.y; c2 = x_.z; c3 = x_.w;                                \
+                    }                                                                              \
+                }                                                                                  \
+                {                                                                                  \
+                    const int q_ = ((k + 2) >> 2) & 3;                                             \
+                    const uint32_t w_ = q_ == 0 ? b0 : q_ == 1 ? b1 : q_ == 2 ? b2 : b3;           \
+                    const uint32_t dn_ = (w_ >> (8 * ((k + 2) & 3))) & 0xffu;                      \
+                    d = (uint32_t)shr1((int32_t)dn_, (int32_t)d);                                  \
+                    pq1 = *(const ProfSlice<RL>*)(prof + d * RP);                                  \
+                }                                                                                  \
+                const int32_t hin = shr1(th, hbot);                                                \
+                const int32_t fin = shr1(tf, fbot);                                                \
+                LONG_ROWS(pcv, hin, fin, tk);                                                      \
+            }                                                                                      \
+        }
+        const int mode = (W > 1 && wr > 0) ? 2 : (p > 0 ? 1 : 0);
+        for (uint32_t sup = 0; sup < nsuper; sup++) {
+            const int tb = 64 * ((int)sup - 2 * (int)wr);
+            const uint32_t tend = (uint32_t)max(0, min(tb + 64, (int)steps));
+            while (t < tend) {
+                if ((t & 15) == 0 && t >= 64 && t + 32 <= n && t + 16 <= tend) {
+                    if (mode == 2) LONG_STEADY(2)
+                    else if (mode == 1) LONG_STEADY(1)
+                    else LONG_STEADY(0)
+                    t += 16;
+                    continue;
+                }
+                // general step (ramp-up, drain): per-lane masks
+                const ProfSlice<RL> pcv = pq0;
+                pq0 = pq1;
+                // lane 0's inputs at column t: the top boundary H(-1, t), F
+                // into row 0 (first pass, wave 0), the previous pass's last
+                // row (wave 0), or wave w-1's last row (ring)
+                int32_t th = 0, tf = 0;
+                if (t < n) {
+                    if (from_scr && (t & 15) == 0 && t > 0) {
+                        row = row_next;
+                        row_next = scr_load(t + 16 + (lane & 15));
+                    }
+                    if (mode == 2) {
+                        // (column t+1 was written a superstep before this one;
+                        // column 0 only once this wave's first superstep began)
+                        if (t == 0) rnext = ring[wr - 1][0];
+                        th = rnext.x;
+                        tf = rnext.y;
+                        if (t + 1 < n) rnext = ring[wr - 1][(t + 1) & (kLongRing - 1)];
+                    } else if (mode == 0) {
+                        if (NW) {
+                            th = Q + ((int32_t)t + 1) * R;
+                            tf = 2 * Q + ((int32_t)t + 2) * R;
+                        }
+                    } else {
+                        th = __builtin_amdgcn_readlane((int32_t)row, t & 15);
+                        tf = __builtin_amdgcn_readlane((int32_t)(row >> 32), t & 15);
+                    }
+                }
+                LONG_ISSUE(t + PF, pq1);
+                const int32_t hin = shr1(th, hbot);
+                const int32_t fin = shr1(tf, fbot);
+                const int j = (int)t - lane;
+                if (lane <= lmax && j >= 0 && j < (int)n) LONG_ROWS(pcv, hin, fin, t);
+                t++;
+            }
+            __syncthreads();
+        }
+#undef LONG_STEADY
+#undef LONG_ROWS
+        if (NW && lastp && wact) {
+            // H(m-1, n-1): the lane holding row m-1 stopped updating after
+            // column n-1
+            const uint32_t rr = m - 1 - i0w;
+            if (rr < RW) {
+                int32_t hs = H[0];
+#pragma unroll
+                for (int r = 1; r < RL; r++) hs = (rr % RL == (uint32_t)r) ? H[r] : hs;
+                score = __builtin_amdgcn_readlane(hs, rr / RL);
+                if (lane == 0) a.scores[a.lane_out[ss]] = score;
+            }
+        }
+    }
+    if (!NW) {
+        for (int x = 32; x > 0; x >>= 1) S = max(S, __shfl_xor(S, x));
+        if (lane == 0) wmax[wave] = S;
+        __syncthreads();
+        if (active && wr == 0 && lane == 0) {
+            int32_t best = 0;
+            for (int k = 0; k < W; k++) best = max(best, wmax[wave + k]);
+            const uint32_t o = a.lane_out[ss];
+            if (o != 0xffffffffu) a.scores[o] = best;
+        }
+    } else if (active && wr == 0 && lane == 0 && n == 0) {
+        const uint32_t o = a.lane_out[ss];
+        if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
+    }
+}
+
+#undef LONG_ISSUE
+
+size_t long_lds_bytes(uint32_t alpha, int w, int rl) { return (size_t)(alpha + 1) * w * 64 * rl * 2; }
+
+template <int W, int RL, bool NW>
 static hipError_t launch_long_t(const LongArgs& a, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)long_kernel<RL, NW>, attr, (int)long_lds_bytes(32, 16));
+    const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW>, attr, (int)long_lds_bytes(32, W, RL));
     if (e != hipSuccess) return e;
-    const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
-    hipLaunchKernelGGL((long_kernel<RL, NW>), dim3(blocks), dim3(64 * kLongWaves), long_lds_bytes(a.alpha, RL), st, a);
+    constexpr int EPW = kLongWaves / W;
+    const uint32_t blocks = (a.nseq + EPW - 1) / EPW;
+    hipLaunchKernelGGL((long_kernel<W, RL, NW>), dim3(blocks), dim3(64 * kLongWaves), long_lds_bytes(a.alpha, W, RL),
+                       st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_long(const LongArgs& a, int rl, bool nw, hipStream_t st) {
+hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st) {
     if (a.nseq == 0) return hipSuccess;
     if (a.alpha > 32) return hipErrorInvalidValue;
+    if (w == 4) {
+        switch (rl) {
+            case 2: return nw ? launch_long_t<4, 2, true>(a, st) : launch_long_t<4, 2, false>(a, st);
+            case 4: return nw ? launch_long_t<4, 4, true>(a, st) : launch_long_t<4, 4, false>(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (w != 1) return hipErrorInvalidValue;
     switch (rl) {
-        case 4: return nw ? launch_long_t<4, true>(a, st) : launch_long_t<4, false>(a, st);
-        case 8: return nw ? launch_long_t<8, true>(a, st) : launch_long_t<8, false>(a, st);
-        case 12: return nw ? launch_long_t<12, true>(a, st) : launch_long_t<12, false>(a, st);
-        case 16: return nw ? launch_long_t<16, true>(a, st) : launch_long_t<16, false>(a, st);
+        case 4: return nw ? launch_long_t<1, 4, true>(a, st) : launch_long_t<1, 4, false>(a, st);
+        case 8: return nw ? launch_long_t<1, 8, true>(a, st) : launch_long_t<1, 8, false>(a, st);
+        case 12: return nw ? launch_long_t<1, 12, true>(a, st) : launch_long_t<1, 12, false>(a, st);
+        case 16: return nw ? launch_long_t<1, 16, true>(a, st) : launch_long_t<1, 16, false>(a, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -236,30 +236,29 @@ def test_query_length_edges_vs_oracle(qlen, algo):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
-@pytest.mark.parametrize("algo", [S.SW, S.NW])
-def test_long_entry_kernel_vs_oracle(qlen, algo):
-    """long_kernel (one wave per entry, query rows over the lanes, passes of
-    up to 1024 rows) on the leading (longest) groups -- forced to 1 and 3 of
-    the 4 groups, and to none -- gives every entry the oracle's score; the
-    DB has entries of 1..4100 residues, empty records and a planted copy of
-    the query."""
+def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None):
     rng = np.random.default_rng(1000 + qlen)
     q = syn.protein_query(qlen, 200 + qlen)
-    lens = np.array([3000, 1, 0, 2500, 17, 64, 4100, qlen + 7] + list(rng.integers(1, 400, 248)), dtype=np.int64)
+    head = [3000, 1, 0, 2500, 17, 64, 4100, qlen + 7] + ([35000, 22000, 20001] if huge else [])
+    lens = np.array(head + list(rng.integers(1, 400, 248)), dtype=np.int64)
     off = np.zeros(len(lens) + 1, np.uint64)
     np.cumsum(lens, out=off[1:])
     codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
     codes[int(off[7]) + 3:int(off[7]) + 3 + qlen] = q           # high-scoring entry
-    codes[int(off[6]) + 100:int(off[6]) + 100 + qlen] = q       # inside the longest one
+    codes[int(off[6]) + 100:int(off[6]) + 100 + qlen] = q       # inside a long one
+    if huge:
+        codes[int(off[8]) + 30000:int(off[8]) + 30000 + qlen] = q
     M = TABLES["matrices"][NAMES.index("blosum62")].copy()
     keep = np.nonzero(lens > 0)[0]
-    exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
-    configure(False, ("builtin", "blosum62"), -11, -1)
+    exp = po.scores(algo, q, codes, off, M, gaps[0], gaps[1])[keep]
+    configure(False, ("builtin", "blosum62"), gaps[0], gaps[1])
     fn = S.sw_align if algo == S.SW else S.nw_align
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        S.set_option("long_waves", waves)
+        if share4 is not None:
+            S.set_option("long4_share_pct", share4)
         try:
             for lg in (1, 3, 0):
                 S.set_option("long_groups", lg)
@@ -270,7 +269,41 @@ def test_long_entry_kernel_vs_oracle(qlen, algo):
                 assert got == po.topk(exp, keep.astype(np.uint64), 10)
         finally:
             S.set_option("long_groups", -1)
+            S.set_option("long_waves", 0)
+            S.set_option("long4_share_pct", 400)
         S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+@pytest.mark.parametrize("waves", [4, 1])
+def test_long_entry_kernel_vs_oracle(qlen, algo, waves):
+    """long_kernel (an entry's query rows over the lanes of 4 waves or of one,
+    passes of up to 1024 rows) on the leading (longest) groups -- forced to 1
+    and 3 of the groups, and to none -- gives every entry the oracle's score;
+    the DB has entries of 1..4100 residues, empty records and planted copies
+    of the query; with 4 waves also entries of 20-35 k residues (UniProt's
+    longest)."""
+    _long_entry_case(qlen, algo, (-11, -1), waves, huge=waves == 4 and qlen in (5, 400, 513, 1025, 2049))
+
+
+@pytest.mark.parametrize("qlen", [5, 400, 1025])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_long_entry_kernel_split_launches(qlen, algo):
+    """Automatic split: the 35 k-residue entry's group at 4 waves per entry
+    (stream 1), the other long groups at one wave per entry (stream 2), both
+    beside the pair kernel."""
+    _long_entry_case(qlen, algo, (-11, -1), 0, huge=True, share4=50000)
+
+
+@pytest.mark.parametrize("gaps", [(0, 0), (-1, -4), (-5, -5), (-20, -7)])
+@pytest.mark.parametrize("qlen", [64, 513])
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_long_entry_kernel_gap_penalties(gaps, qlen, algo):
+    """long_kernel's SW clamps E and F at 0 (exact for R <= 0) and its NW is
+    the plain recurrence: zero, steep and unequal gap penalties against the
+    oracle."""
+    _long_entry_case(qlen, algo, gaps, 4, huge=False)
 
 
 @pytest.mark.parametrize("match", [40, 55, 127])
@@ -1113,3 +1146,29 @@ def test_residue_classes_follow_the_query(tmp_path):
             assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.search(algo, q, seqs, M, -11, -1, 10)
             assert S.stats()["kernel"].startswith("pair"), S.stats()["kernel"]
         S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("qlen", [50, 300])
+def test_overflow_counters_long_nw_entries(qlen, tmp_path):
+    """NW with -10/-2 gaps: entries of 15-20 k residues cross the 16-bit flag
+    threshold along the top boundary (the device replays those row by row and
+    stops in the first row), shorter ones are decided from bounds or replayed
+    column by column; widths 8 and 16 against the oracle's column-major
+    replay of the reference's saturated kernels."""
+    rng = np.random.default_rng(qlen)
+    q = syn.protein_query(qlen, 5)
+    lens = [10, 60, 61, 200, 1000, 15000, 16300, 16390, 16400, 17000, 20000] + list(rng.integers(1, 3000, 30))
+    seqs = [rng.choice(syn.AA_CODES, int(n)).astype(np.uint8) for n in lens]
+    db, off = po.pack_db(seqs)
+    configure(False, ("builtin", "blosum62"), -10, -2)
+    S.init_db(_write_db(str(tmp_path), db, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    flags = po.overflow_flags(1, q, db, off, M, -10, -2)
+    exp_hits = po.search(1, q, seqs, M, -10, -2, 5)
+    for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
+        assert [(h["score"], h["id"]) for h in S.nw_align(qq, 5, width)] == exp_hits
+        st = S.stats()
+        o8, o16 = po.overflow_counts(width, flags)
+        assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    S.free_sequence(qq)
