@@ -13,6 +13,7 @@
 // round's counts, so the ranks never disagree on the collective sequence.
 // Rank 0 then replays the logs in rank (= ID) order through the reference
 // heap: the 64-bit single-thread result, ties included.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -45,8 +46,46 @@ DistState& ds() {
     return s;
 }
 
+// RCCL is resolved at run time, not linked: a Python host that imported
+// torch first already holds torch's librccl.so.1 (same soname), and dlopen
+// by soname returns that instance, so the library and the process group
+// share one RCCL; a plain C caller gets the system's (/opt/rocm/lib).
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false;
+    if (tried) return r.comm_init_rank ? &r : nullptr;
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        print_error("RCCL not found (librccl.so.1): %s", dlerror());
+        return nullptr;
+    }
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.gather = (decltype(r.gather))dlsym(h, "ncclGather");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_gather || !r.gather || !r.error_string) {
+        print_error("RCCL lacks a required symbol");
+        r = Rccl();
+        return nullptr;
+    }
+    return &r;
+}
+
 void nccl_check(ncclResult_t r, const char* what) {
-    if (r != ncclSuccess) fatal("RCCL error in %s: %s", what, ncclGetErrorString(r));
+    if (r != ncclSuccess) fatal("RCCL error in %s: %s", what, rccl()->error_string(r));
 }
 
 constexpr size_t slot_bytes() { return (kSlotRows + 1) * kRow; }
@@ -61,9 +100,10 @@ using namespace ssa;
 extern "C" {
 
 int ssa_amd_dist_unique_id(void* id) {
-    if (!id) return 1;
+    const Rccl* R = rccl();
+    if (!id || !R) return 1;
     ncclUniqueId u;
-    if (ncclGetUniqueId(&u) != ncclSuccess) return 1;
+    if (R->get_unique_id(&u) != ncclSuccess) return 1;
     memcpy(id, &u, sizeof u);
     return 0;
 }
@@ -72,6 +112,8 @@ size_t ssa_amd_dist_unique_id_bytes(void) { return sizeof(ncclUniqueId); }
 
 int ssa_amd_dist_init(int rank, int world, const void* id) {
     DistState& S = ds();
+    const Rccl* R = rccl();
+    if (!R) return 1;
     if (S.comm) {
         print_error("ssa_amd_dist_init: already initialised (call ssa_amd_dist_finalize first)");
         return 1;
@@ -85,7 +127,7 @@ int ssa_amd_dist_init(int rank, int world, const void* id) {
     if (hipSetDevice(dev) != hipSuccess) return 1;
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
-    if (ncclCommInitRank(&S.comm, world, u, rank) != ncclSuccess) {
+    if (R->comm_init_rank(&S.comm, world, u, rank) != ncclSuccess) {
         S.comm = nullptr;
         return 1;
     }
@@ -104,7 +146,7 @@ void ssa_amd_dist_finalize(void) {
     if (!S.comm) return;
     (void)hipSetDevice(S.device);
     (void)hipStreamSynchronize(S.stream);
-    (void)ncclCommDestroy(S.comm);
+    (void)rccl()->comm_destroy(S.comm);
     (void)hipFree(S.d_send);
     (void)hipFree(S.d_recv);
     (void)hipFree(S.d_big_send);
@@ -143,7 +185,7 @@ size_t ssa_amd_gather_logs(const ssa_hit_t* log, size_t n, size_t hitcount, ssa_
     if (n) memcpy(mine + kRow, log, std::min(n, kSlotRows) * kRow);
     check(hipMemcpyAsync(S.d_send, mine, kRow * (1 + std::min(n, kSlotRows)), hipMemcpyHostToDevice, S.stream),
           "H2D log");
-    nccl_check(ncclAllGather(S.d_send, S.d_recv, slot_bytes(), ncclUint8, S.comm, S.stream), "ncclAllGather");
+    nccl_check(rccl()->all_gather(S.d_send, S.d_recv, slot_bytes(), ncclUint8, S.comm, S.stream), "ncclAllGather");
     check(hipMemcpyAsync(S.h_buf, S.d_recv, slot_bytes() * W, hipMemcpyDeviceToHost, S.stream), "D2H logs");
     check(hipStreamSynchronize(S.stream), "gather");
     std::vector<size_t> counts(W);
@@ -168,7 +210,8 @@ size_t ssa_amd_gather_logs(const ssa_hit_t* log, size_t n, size_t hitcount, ssa_
         check(hipMalloc((void**)&S.d_big_recv, S.rank == 0 ? longest * kRow * W : kRow), "gather receive");
     }
     if (n) check(hipMemcpyAsync(S.d_big_send, log, n * kRow, hipMemcpyHostToDevice, S.stream), "H2D log");
-    nccl_check(ncclGather(S.d_big_send, S.d_big_recv, longest * kRow, ncclUint8, 0, S.comm, S.stream), "ncclGather");
+    nccl_check(rccl()->gather(S.d_big_send, S.d_big_recv, longest * kRow, ncclUint8, 0, S.comm, S.stream),
+               "ncclGather");
     std::vector<ssa_hit_t> all(S.rank == 0 ? longest * W : 0);
     if (S.rank == 0)
         check(hipMemcpyAsync(all.data(), S.d_big_recv, longest * kRow * W, hipMemcpyDeviceToHost, S.stream),
