@@ -45,10 +45,29 @@ __device__ __forceinline__ int32_t trunc_w(int64_t v, int w) {
 
 __device__ __forceinline__ int32_t sat_w(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// -1: undecided (replay), else the flag
-__device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint32_t len) {
+// -1: undecided (replay), else the flag.  hmm: the exact (min, max) of H
+// over the lane's real cells when long_kernel scored it (NW), else null.
+__device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint32_t len, const int2* hmm) {
     if (!((a.ordinary >> (w == 8 ? 0 : 1)) & 1) || s == INT32_MIN) return -1;
     const int64_t IMIN = -(1ll << (w - 1)), IMAX = (1ll << (w - 1)) - 1;
+    if (a.nw && hmm) {
+        // exact extremes: when no boundary chain of the saturated run leaves
+        // int_w (H(-1,j), F into row 0, H(i,-1), E into column 0 all >= 2Q +
+        // (max(m, n4) + 2)R), the saturated run equals the exact one up to the
+        // first cell below T or at I_MAX (earlier values never saturate where
+        // it matters), and there the saturated value is <= max(exact, I_MIN) <
+        // T or == I_MAX -- so a real cell beyond the limits decides "flagged";
+        // padding cells (code 0, at most 3 columns) lie within [min + Q + 3R,
+        // max + 3 padmax], so real extremes that far inside decide "clear"
+        const int64_t n4 = (len + 3) & ~3u;
+        const int64_t Q = a.gap_open, R = a.gap_extend;
+        const int64_t T = IMIN - Q - R - 1;
+        if (2 * Q + ((int64_t)max((int64_t)a.m, n4) + 2) * R >= IMIN) {
+            const int2 mm = *hmm;
+            if (mm.x < T || mm.y >= IMAX || s <= IMIN || s >= IMAX) return 1;
+            if ((int64_t)mm.x + Q + 3 * R >= T && (int64_t)mm.y + 3ll * a.padmax < IMAX) return 0;
+        }
+    }
     if (!a.nw) {
         const int64_t lim = (1ll << w) - 1;
         if (s >= lim) return 1;
@@ -80,7 +99,7 @@ __global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
     bool undecided = false;
     for (int b = 0; b < 2; b++) {
         if (!((a.widths >> b) & 1)) continue;
-        const int d = decide(a, b ? 16 : 8, s, len);
+        const int d = decide(a, b ? 16 : 8, s, len, gl < a.hmm_lanes ? a.hmm + gl : nullptr);
         if (d < 0) undecided = true;
         else f |= (uint32_t)d << b;
     }
@@ -235,7 +254,7 @@ __device__ int replay_nw_rows(const FlagArgs& a, const LaneSeq& d, int w, int32_
     const int32_t QR = trunc_w(Q + R0, w), R = trunc_w(R0, w);
     const int32_t T = trunc_w(IMIN - Q - R0 - 1, w);
     const uint32_t m = a.m, n4 = (d.len + 3) & ~3u;
-    int32_t hmin = 0, hmax = 0, score = 0;
+    int32_t score = 0;
     int32_t Lprev = 0;                                   // H(i-1, -1); row 0: H(-1,-1) = 0
     int32_t L = QR;                                      // H(i, -1)
     for (uint32_t i = 0; i < m; i++) {
@@ -243,7 +262,11 @@ __device__ int replay_nw_rows(const FlagArgs& a, const LaneSeq& d, int w, int32_
         int32_t diag = Lprev;                            // H(i-1, j-1) for j = 0
         int32_t E = sat_w(L + QR, IMIN, IMAX);           // E into column 0
         int32_t top = 0, Ft = 0;                         // row 0: H(-1, j-1) chain and Ft chain
+        // the next column's profile value is fetched one column ahead
+        int32_t vnext = trunc_w(d.row(a, 0)[qc], w);
         for (uint32_t j = 0; j < n4; j++) {
+            const int32_t v = vnext;
+            if (j + 1 < n4) vnext = trunc_w(d.row(a, j + 1)[qc], w);
             int32_t Fin, up;
             if (i == 0) {
                 // H(-1, j) (the next column's diagonal) and F into row 0
@@ -256,11 +279,10 @@ __device__ int replay_nw_rows(const FlagArgs& a, const LaneSeq& d, int w, int32_
                 Fin = hep[(size_t)(2 * j + 1) * stride];
                 up = hep[(size_t)(2 * j) * stride];
             }
-            int32_t H = sat_w(diag + trunc_w(d.row(a, j)[qc], w), IMIN, IMAX);
+            int32_t H = sat_w(diag + v, IMIN, IMAX);
             H = max(H, Fin);
             H = max(H, E);
-            hmin = min(hmin, H);
-            hmax = max(hmax, H);
+            if (H < T || H == IMAX) return 1;            // decided: the flag is an OR
             if (i + 1 == m && j + 1 == d.len) score = H;
             const int32_t t = sat_w(H + QR, IMIN, IMAX);
             hep[(size_t)(2 * j + 1) * stride] = max(sat_w(Fin + R, IMIN, IMAX), t);
@@ -268,7 +290,6 @@ __device__ int replay_nw_rows(const FlagArgs& a, const LaneSeq& d, int w, int32_
             E = max(sat_w(E + R, IMIN, IMAX), t);
             diag = up;
         }
-        if (hmin < T || hmax == IMAX) return 1;
         Lprev = L;
         L = sat_w(L + R, IMIN, IMAX);
     }

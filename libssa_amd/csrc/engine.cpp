@@ -47,6 +47,9 @@ void DeviceDB::release() {
     dfree(d_work); dfree(d_order); dfree(d_lscratch);
     dfree(d_flags); dfree(d_flist); dfree(d_cnt); dfree(d_res_cls); dfree(d_frlist); dfree(d_frwork);
     d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
+    dfree(d_hmm);
+    d_hmm = nullptr;
+    hmm_cap = 0;
     d_res_cls = nullptr;
     cls_key.clear();
     if (h_cnt) (void)hipHostFree(h_cnt);
@@ -1150,6 +1153,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             la.alpha = A;
             la.gap_open = Q;
             la.gap_extend = R;
+            if (want_counts && nw) {
+                // the exact extremes the NW overflow counters decide from
+                if (D.hmm_cap < (size_t)long_groups * 64) {
+                    check(hipStreamSynchronize(D.stream_long), "sync");
+                    check(hipStreamSynchronize(D.stream_long1), "sync");
+                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                    dfree(D.d_hmm);
+                    check(hipMalloc((void**)&D.d_hmm, (size_t)long_groups * 64 * sizeof(int2)), "long-entry extremes");
+                    D.hmm_cap = (size_t)long_groups * 64;
+                }
+                la.hmm = D.d_hmm;
+            }
             const int rl4 = m <= 512 ? 2 : 4;
             const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
             if (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1) {
@@ -1254,6 +1269,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             fa.ordinary = ordinary;
             fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
             fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
+            if (nw && long_groups > 0) {
+                fa.hmm = D.d_hmm;
+                fa.hmm_lanes = long_groups * 64;
+            }
             if (nw && D.ngroups > 0) {
                 // row-major NW replay: scratch for the longest entry's
                 // columns, 64..1024 lanes within 64 MiB

@@ -87,6 +87,8 @@ struct DeviceDB {
     uint32_t* d_frlist = nullptr;         // the same for the row-major NW replay
     int32_t* d_frwork = nullptr;          // its scratch
     size_t frwork_cap = 0;                // int32 elements
+    int2* d_hmm = nullptr;                // NW long entries: exact (min, max) of H per lane
+    size_t hmm_cap = 0;                   // lanes
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
     unsigned long long* h_cnt = nullptr;  // pinned mirror
     // long entries (long_kernel, launched on stream_long beside the pair

@@ -58,6 +58,8 @@ struct LongArgs {
     int64_t* scratch;          // [nseq][stride] (H, F) of a pass's last row (multi-pass only)
     uint32_t stride;
     uint32_t seq0, nseq;       // entries served: lanes [seq0, seq0 + nseq) of the group order
+    int2* hmm;                 // NW: per lane (min, max) of H over the entry's real cells, or null
+                               // (the overflow counters' exact decision, counters.hip)
     uint32_t m, alpha;
     int32_t gap_open, gap_extend;
 };
@@ -155,6 +157,9 @@ struct FlagArgs {
     int32_t ordinary;          // bit 0/1: 8/16-bit decidable from exact values (host-checked regime)
     int32_t maxm;              // max(0, M over the DB's codes and code 0 x the query's residues)
     int32_t padmax;            // max(0, max_i M[0][q_i])
+    // NW lanes [0, hmm_lanes) scored by long_kernel: exact (min, max) of H
+    const int2* hmm;
+    uint32_t hmm_lanes;
 };
 hipError_t launch_flags(const FlagArgs& a, hipStream_t st);
 

@@ -1137,7 +1137,7 @@ template <int W, int RL, bool NW>
 __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
     extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][RP] profile of the pass
     __shared__ int2 ring[W > 1 ? W - 1 : 1][W > 1 ? kLongRing : 1];
-    __shared__ int32_t wmax[kLongWaves];
+    __shared__ int32_t wmax[kLongWaves], wlo[kLongWaves];
     constexpr int EPW = kLongWaves / W;              // entries per workgroup
     constexpr uint32_t RW = 64 * RL;                 // rows per wave
     constexpr uint32_t RP = W * RW;                  // rows per pass
@@ -1168,6 +1168,9 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     }
     const uint32_t nsuper = (nmax + 63 + 63) / 64 + 2 * (W - 1);
     int32_t S = 0, score = 0;
+    // NW: the min and max of H over the entry's real cells (rows < m), kept
+    // per row of the lane (rows past the query are dropped at the pass's end)
+    int32_t lmin = INT32_MAX, lmax_h = INT32_MIN;
     for (uint32_t p = 0; p < npass; p++) {
         const uint32_t i0p = p * RP;
         // the pass's profile [code][row] (padding code and rows: -4096); the
@@ -1191,11 +1194,13 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         const bool feeds_scratch = !lastp && wr + 1 == W;
         const int16_t* prof = ltab + (i0 - i0p);          // + code * RP
         // left boundary: H(i, -1) and E into column 0
-        int32_t H[RL], E[RL];
+        int32_t H[RL], E[RL], hlo[RL], hhi[RL];
 #pragma unroll
         for (int r = 0; r < RL; r++) {
             H[r] = NW ? Q + (i0 + r + 1) * R : 0;
             E[r] = NW ? 2 * Q + (i0 + r + 2) * R : 0;
+            hlo[r] = INT32_MAX;
+            hhi[r] = INT32_MIN;
         }
         int32_t hdiag = NW ? (i0 == 0 ? 0 : Q + i0 * R) : 0;   // H(i0-1, -1)
         int32_t hbot = 0, fbot = 0;
@@ -1271,6 +1276,10 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
                 const int32_t up_ = H[r_];                                                         \
                 const int32_t h_ = max(max(hd_ + P_[r_], E[r_]), f_);                              \
                 if (!NW) S = max(S, h_);                                                           \
+                if (NW) {                                                                          \
+                    hlo[r_] = min(hlo[r_], h_);                                                    \
+                    hhi[r_] = max(hhi[r_], h_);                                                    \
+                }                                                                                  \
                 H[r_] = h_;                                                                        \
                 const int32_t tt_ = h_ + QR;                                                       \
                 E[r_] = NW ? max(E[r_] + R, tt_) : max(max(E[r_] + R, tt_), 0);                    \
@@ -1279,6 +1288,10 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
             }                                                                                      \
             /* one step at a time (unrolled, the compiler defers the max chain and hoists work) */ \
             if (!NW) asm volatile("" : "+v"(S));                                                   \
+            if (NW) {                                                                              \
+                _Pragma("unroll") for (int r_ = 0; r_ < RL; r_++)                                  \
+                    asm volatile("" : "+v"(hlo[r_]), "+v"(hhi[r_]));                               \
+            }                                                                                      \
             asm volatile("" : "+v"(f_));                                                           \
             hdiag = (hin);                                                                         \
             hbot = H[RL - 1];                                                                      \
@@ -1393,6 +1406,14 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         }
 #undef LONG_STEADY
 #undef LONG_ROWS
+        if (NW && wact) {
+#pragma unroll
+            for (int r = 0; r < RL; r++)
+                if (i0 + r < (int)m) {
+                    lmin = min(lmin, hlo[r]);
+                    lmax_h = max(lmax_h, hhi[r]);
+                }
+        }
         if (NW && lastp && wact) {
             // H(m-1, n-1): the lane holding row m-1 stopped updating after
             // column n-1
@@ -1416,9 +1437,30 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
             const uint32_t o = a.lane_out[ss];
             if (o != 0xffffffffu) a.scores[o] = best;
         }
-    } else if (active && wr == 0 && lane == 0 && n == 0) {
-        const uint32_t o = a.lane_out[ss];
-        if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
+    } else {
+        if (active && wr == 0 && lane == 0 && n == 0) {
+            const uint32_t o = a.lane_out[ss];
+            if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
+        }
+        if (a.hmm) {
+            for (int x = 32; x > 0; x >>= 1) {
+                lmin = min(lmin, __shfl_xor(lmin, x));
+                lmax_h = max(lmax_h, __shfl_xor(lmax_h, x));
+            }
+            if (lane == 0) {
+                wlo[wave] = lmin;
+                wmax[wave] = lmax_h;
+            }
+            __syncthreads();
+            if (active && wr == 0 && lane == 0) {
+                int32_t lo = INT32_MAX, hi = INT32_MIN;
+                for (int k = 0; k < W; k++) {
+                    lo = min(lo, wlo[wave + k]);
+                    hi = max(hi, wmax[wave + k]);
+                }
+                a.hmm[ss] = make_int2(lo, hi);
+            }
+        }
     }
 }
 
