@@ -41,7 +41,9 @@ static void dfree(void* p) {
 }
 
 void DeviceDB::release() {
-    if (device >= 0) (void)hipSetDevice(device);
+    // the buffers belong to `device`: free them there (a failure here means
+    // the device is gone -- fatal, as every other HIP error of the library)
+    if (device >= 0) check(hipSetDevice(device), "hipSetDevice");
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch);
