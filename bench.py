@@ -62,7 +62,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="c2", choices=list(CONFIGS))
-    p.add_argument("--seqs", type=int, default=None, help="DB sequences per GPU (default: the config's)")
+    p.add_argument("--seqs", type=int, default=None,
+                   help="DB sequences per GPU (weak configs) or each GPU's share of the fixed DB (C4/C5)")
     p.add_argument("--qlen", type=int, default=None)
     p.add_argument("--algo", default=None, choices=["sw", "nw"])
     p.add_argument("--matrix", default=None)
@@ -207,14 +208,18 @@ def make_shard(args, cfg, rank, world):
     an N x seqs DB, 1 M per rank; strong ones (C4/C5): the fixed 10 M / 50 M DB
     cut into N ID ranges, so every N searches the same DB.  At N = 1 C2 and C3
     are exactly tests/golden/fullsize.json's c2/c3 DBs.
+    --seqs: the per-rank sequence count of a weak config's DB, or the per-rank
+    share of a strong config's fixed DB.
     Returns (query, codes, offsets, first global ID, DB size)."""
     from libssa_amd import synthetic as syn
-    if args.seqs is not None or cfg["total_seqs"] is None:
+    if cfg["total_seqs"] is None:
         per = args.seqs if args.seqs is not None else cfg["seqs"]
         total = per * world
     else:
+        # strong: --seqs is this rank's share of the fixed DB (C4: the first
+        # 1.25 M of the 10 M DB at N = 1 is the c4 fixture's share)
         total = cfg["total_seqs"]
-        per = (total + world - 1) // world
+        per = args.seqs if args.seqs is not None else (total + world - 1) // world
     i0 = min(total, rank * per)
     i1 = min(total, i0 + per)
     if args.db == "dna":

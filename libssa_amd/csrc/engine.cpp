@@ -1130,6 +1130,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         check(hipEventRecord(ev_k0, st), "event");
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
+        bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
         if (long_groups > 0) {
             // the longest groups on their own streams, concurrently with the
             // pair kernel (enqueued first, so their waves start first): one
@@ -1155,8 +1156,19 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             la.alpha = A;
             la.gap_open = Q;
             la.gap_extend = R;
+            // NW: the exact extremes of H the overflow counters decide from,
+            // needed only when some long entry is too long for the bounds
+            // (2Q + (m + n4)R below the flag threshold; counters.hip)
+            bool need_hmm = false;
             if (want_counts && nw) {
-                // the exact extremes the NW overflow counters decide from
+                const int64_t n4max = (int64_t)D.group_ncols[0];
+                for (int b = 0; b < 2; b++) {
+                    const int64_t imin = b ? -32768 : -128;
+                    if (((bw == BIT_WIDTH_8) || b == 1) && 2 * (int64_t)Q + ((int64_t)m + n4max) * R < imin - Q - R - 1)
+                        need_hmm = true;
+                }
+            }
+            if (need_hmm) {
                 if (D.hmm_cap < (size_t)long_groups * 64) {
                     check(hipStreamSynchronize(D.stream_long), "sync");
                     check(hipStreamSynchronize(D.stream_long1), "sync");
@@ -1166,6 +1178,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                     D.hmm_cap = (size_t)long_groups * 64;
                 }
                 la.hmm = D.d_hmm;
+                long_hmm = true;
             }
             const int rl4 = m <= 512 ? 2 : 4;
             const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
@@ -1271,7 +1284,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             fa.ordinary = ordinary;
             fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
             fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
-            if (nw && long_groups > 0) {
+            if (nw && long_groups > 0 && long_hmm) {
                 fa.hmm = D.d_hmm;
                 fa.hmm_lanes = long_groups * 64;
             }

@@ -1133,8 +1133,9 @@ struct ProfSlice {
     uint32_t v[RL / 2];
 };
 
-template <int W, int RL, bool NW>
+template <int W, int RL, bool NW, bool TRK>
 __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
+    static_assert(!TRK || NW, "extremes are an NW counter input");
     extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][RP] profile of the pass
     __shared__ int2 ring[W > 1 ? W - 1 : 1][W > 1 ? kLongRing : 1];
     __shared__ int32_t wmax[kLongWaves], wlo[kLongWaves];
@@ -1276,7 +1277,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
                 const int32_t up_ = H[r_];                                                         \
                 const int32_t h_ = max(max(hd_ + P_[r_], E[r_]), f_);                              \
                 if (!NW) S = max(S, h_);                                                           \
-                if (NW) {                                                                          \
+                if (TRK) {                                                                         \
                     hlo[r_] = min(hlo[r_], h_);                                                    \
                     hhi[r_] = max(hhi[r_], h_);                                                    \
                 }                                                                                  \
@@ -1288,7 +1289,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
             }                                                                                      \
             /* one step at a time (unrolled, the compiler defers the max chain and hoists work) */ \
             if (!NW) asm volatile("" : "+v"(S));                                                   \
-            if (NW) {                                                                              \
+            if (TRK) {                                                                             \
                 _Pragma("unroll") for (int r_ = 0; r_ < RL; r_++)                                  \
                     asm volatile("" : "+v"(hlo[r_]), "+v"(hhi[r_]));                               \
             }                                                                                      \
@@ -1406,7 +1407,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         }
 #undef LONG_STEADY
 #undef LONG_ROWS
-        if (NW && wact) {
+        if (TRK && wact) {
 #pragma unroll
             for (int r = 0; r < RL; r++)
                 if (i0 + r < (int)m) {
@@ -1442,7 +1443,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
             const uint32_t o = a.lane_out[ss];
             if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
         }
-        if (a.hmm) {
+        if (TRK) {
             for (int x = 32; x > 0; x >>= 1) {
                 lmin = min(lmin, __shfl_xor(lmin, x));
                 lmax_h = max(lmax_h, __shfl_xor(lmax_h, x));
@@ -1468,16 +1469,25 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
 
 size_t long_lds_bytes(uint32_t alpha, int w, int rl) { return (size_t)(alpha + 1) * w * 64 * rl * 2; }
 
-template <int W, int RL, bool NW>
-static hipError_t launch_long_t(const LongArgs& a, hipStream_t st) {
+template <int W, int RL, bool NW, bool TRK>
+static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW>, attr, (int)long_lds_bytes(32, W, RL));
+    const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW, TRK>, attr, (int)long_lds_bytes(32, W, RL));
     if (e != hipSuccess) return e;
     constexpr int EPW = kLongWaves / W;
     const uint32_t blocks = (a.nseq + EPW - 1) / EPW;
-    hipLaunchKernelGGL((long_kernel<W, RL, NW>), dim3(blocks), dim3(64 * kLongWaves), long_lds_bytes(a.alpha, W, RL),
-                       st, a);
+    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(blocks), dim3(64 * kLongWaves),
+                       long_lds_bytes(a.alpha, W, RL), st, a);
     return hipGetLastError();
+}
+
+// NW with a.hmm: the variant that also keeps each entry's extremes of H
+template <int W, int RL, bool NW>
+static hipError_t launch_long_t(const LongArgs& a, hipStream_t st) {
+    if constexpr (NW) {
+        if (a.hmm) return launch_long_k<W, RL, true, true>(a, st);
+    }
+    return launch_long_k<W, RL, NW, false>(a, st);
 }
 
 hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st) {

@@ -1148,8 +1148,9 @@ def test_residue_classes_follow_the_query(tmp_path):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [50, 300])
-def test_overflow_counters_long_nw_entries(qlen, tmp_path):
+@pytest.mark.parametrize("qlen", [50, 300, 700])
+@pytest.mark.parametrize("waves", [0, 1])
+def test_overflow_counters_long_nw_entries(qlen, waves, tmp_path):
     """NW with -10/-2 gaps: entries of 15-20 k residues cross the 16-bit flag
     threshold along the top boundary (the device replays those row by row and
     stops in the first row), shorter ones are decided from bounds or replayed
@@ -1166,9 +1167,13 @@ def test_overflow_counters_long_nw_entries(qlen, tmp_path):
     M = TABLES["matrices"][NAMES.index("blosum62")].copy()
     flags = po.overflow_flags(1, q, db, off, M, -10, -2)
     exp_hits = po.search(1, q, seqs, M, -10, -2, 5)
-    for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
-        assert [(h["score"], h["id"]) for h in S.nw_align(qq, 5, width)] == exp_hits
-        st = S.stats()
-        o8, o16 = po.overflow_counts(width, flags)
-        assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    S.set_option("long_waves", waves)
+    try:
+        for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
+            assert [(h["score"], h["id"]) for h in S.nw_align(qq, 5, width)] == exp_hits
+            st = S.stats()
+            o8, o16 = po.overflow_counts(width, flags)
+            assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    finally:
+        S.set_option("long_waves", 0)
     S.free_sequence(qq)
