@@ -173,12 +173,16 @@ def cpu_baseline(codes, off, q, M, args):
     n = len(off) - 1
     if po.have_ref():
         cells_per_seq = float(off[-1]) / n * len(q)
+        # the reference's search at the config's width: int16, or for width 8
+        # its int8 kernel with the int16/int64 cascade (search_8.c:94-124)
+        mode = po.MODE_SEARCH8_AVX2 if args.width == 8 else po.MODE_SEARCH16_AVX2
+        kname = "AVX2 int8 search_8 cascade" if args.width == 8 else "AVX2 int16 search_16_chunk"
 
         def run(threads, seconds):
             # sample sized to ~seconds at a conservative 8 GCUPS per thread
             sample = int(min(n, max(1000, seconds * 8e9 * threads / cells_per_seq)))
             soff = off[:sample + 1]
-            _, _, _, secs = po.ref_run(po.MODE_SEARCH16_AVX2, algo, q, None, M, args.gap_open, args.gap_extend,
+            _, _, _, secs = po.ref_run(mode, algo, q, None, M, args.gap_open, args.gap_extend,
                                        k=args.k, threads=threads, repeat=2, db_off=(codes, soff))
             cells = float(soff[-1]) * len(q)
             return cells / secs / 1e9, sample, cells
@@ -187,8 +191,8 @@ def cpu_baseline(codes, off, q, M, args):
         v1, sample1, _ = run(1, args.cpu_seconds * 0.3)
         return {"value": v, "unit": "GCUPS", "cores": cores, "kind": "reference",
                 "one_thread_gcups": v1, "cpu_model": model, "host_share": share,
-                "sample": f"first {sample} of {n} DB sequences ({cells:.3g} cells), reference AVX2 int16 "
-                          f"search_16_chunk on {cores} threads (best of 2), chunk 1000, k={args.k}; one thread: "
+                "sample": f"first {sample} of {n} DB sequences ({cells:.3g} cells), reference {kname} "
+                          f"on {cores} threads (best of 2), chunk 1000, k={args.k}; one thread: "
                           f"first {sample1} sequences"}
     po.build(quiet=True)
     sample = 2000

@@ -368,7 +368,8 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     D.ovf_slices = 1;
     dalloc((void**)&D.d_flist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
     dalloc((void**)&D.d_frlist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
-    dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe, "overflow counters");
+    // overflow counters, then the long-entry dispatch gate (TableArgs::gate)
+    dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe + 16, "overflow counters");
     check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe, hipHostMallocDefault), "pinned");
     D.upblk_cap = kUpHeader + 16384 + 4096;
     dalloc((void**)&D.d_upblk, D.upblk_cap, "per-search uploads");
@@ -726,14 +727,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     // flags, summed on the device after the last view
     const bool want_counts = bw != BIT_WIDTH_64 && E > 0 && V > 0;
     bool counted = false;
-    if (want_counts) {
-        if (D.flags_cap < V * E) {
-            dfree(D.d_flags);
-            check(hipMalloc((void**)&D.d_flags, V * E), "overflow flags");
-            D.flags_cap = V * E;
-        }
-        check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe, D.stream), "memset");
+    if (want_counts && D.flags_cap < V * E) {
+        dfree(D.d_flags);
+        check(hipMalloc((void**)&D.d_flags, V * E), "overflow flags");
+        D.flags_cap = V * E;
     }
+    // counters and the long-entry dispatch gate start at 0
+    uint32_t* const gate = (uint32_t*)(D.d_cnt + 2 * kMaxBatchPipe);
+    uint32_t gate_total = 0, gate_base = 0;   // long workgroups launched in all views / before this view
+    if (E > 0) check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe + 16, D.stream), "memset");
     // single query view and a small k: only heap-changing candidates come back
     const double t_prep0 = now_ms();
     double prep = 0, sync_wait = 0;
@@ -1194,9 +1196,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
                 la.scratch = D.d_lscratch;
             }
+            la.gate = gate;
+            gate_base = gate_total;
             if (long4 > 0) {
                 la.seq0 = 0;
                 la.nseq = long4 * 64;
+                gate_total += la.nseq;                         // one workgroup per entry
                 check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
                 check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
                 check(hipEventRecord(D.ev[7], D.stream_long), "event");
@@ -1204,6 +1209,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (long4 < long_groups) {
                 la.seq0 = long4 * 64;
                 la.nseq = (long_groups - long4) * 64;
+                gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
                 check(hipEventRecord(D.ev[6], D.stream_long1), "event");
@@ -1226,6 +1232,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
             ta.zero = ovf;
+            if (long_groups > 0) {
+                // (at most the first 512 workgroups: more may not all fit the
+                // chip at once, and the rest follow the first in order)
+                ta.gate = gate;
+                ta.gate_target = std::min<uint32_t>(gate_total, gate_base + 512);
+            }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {
             check(hipMemsetAsync(ovf, 0, 4, st), "memset");

@@ -58,6 +58,7 @@ struct LongArgs {
     int64_t* scratch;          // [nseq][stride] (H, F) of a pass's last row (multi-pass only)
     uint32_t stride;
     uint32_t seq0, nseq;       // entries served: lanes [seq0, seq0 + nseq) of the group order
+    uint32_t* gate;            // every workgroup increments it when it starts (TableArgs::gate)
     int2* hmm;                 // NW: per lane (min, max) of H over the entry's real cells, or null
                                // (the overflow counters' exact decision, counters.hip)
     uint32_t m, alpha;
@@ -199,6 +200,11 @@ struct TableArgs {
     int32_t rel;               // added to every real profile value (-2R)
     uint32_t pad;              // 16-bit padding value
     uint32_t* zero;            // cleared by thread 0 (the search's overflow count), may be null
+    // dispatch gate (null: none): block 0 waits, bounded, until gate_target
+    // long_kernel workgroups have started, so the pair kernel that follows
+    // on the stream cannot fill the CUs before the long entries are placed
+    const uint32_t* gate;
+    uint32_t gate_target;
 };
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
 

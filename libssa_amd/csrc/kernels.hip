@@ -1026,6 +1026,15 @@ __device__ __forceinline__ int32_t table_val(const TableArgs& a, uint32_t c, uin
 
 __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
     if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;
+    if (a.gate && blockIdx.x == 0 && threadIdx.x == 0) {
+        // the long entries' workgroups (another stream) start first; bounded
+        // at ~20 ms of the 100 MHz real-time counter, so a gate that is never
+        // reached only costs time, never a hang
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.gate_target &&
+               __builtin_amdgcn_s_memrealtime() - t0 < 2000000ull)
+            __builtin_amdgcn_s_sleep(8);
+    }
     const uint32_t prow = a.alpha + 1;
     const uint32_t per_main = prow * prow * a.np;
     const uint32_t nmain = a.nmain * per_main;
@@ -1146,6 +1155,8 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     // these waves are the launch's critical path: they issue before the
     // pair kernel's waves sharing their SIMD
     __builtin_amdgcn_s_setprio(3);
+    if (a.gate && threadIdx.x == 0)
+        __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t wr = wave % W;                    // rank of the wave inside its entry

@@ -11,7 +11,7 @@ run() {   # name, args...
 }
 run c2 --steps 10 &&
 run c3 --config c3 --steps 5 &&
-run c4share --config c4 --seqs 1250000 --steps 10 --no-cpu-baseline &&
+run c4share --config c4 --seqs 1250000 --steps 10 &&
 run c5share1m --config c5 --seqs 1000000 --steps 3 --no-cpu-baseline &&
 run c5share --config c5 --seqs 6250000 --steps 2 --warmup 1 &&
 run ref --config ref --steps 5 --no-cpu-baseline &&
