@@ -47,7 +47,8 @@ __device__ __forceinline__ int32_t sat_w(int32_t v, int32_t lo, int32_t hi) { re
 
 // -1: undecided (replay), else the flag.  hmm: the exact (min, max) of H
 // over the lane's real cells when long_kernel scored it (NW), else null.
-__device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint32_t len, const int2* hmm) {
+__device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint32_t len, const int2* hmm,
+                                      bool long_lane) {
     if (!((a.ordinary >> (w == 8 ? 0 : 1)) & 1) || s == INT32_MIN) return -1;
     const int64_t IMIN = -(1ll << (w - 1)), IMAX = (1ll << (w - 1)) - 1;
     if (a.nw && hmm) {
@@ -79,7 +80,11 @@ __device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint3
     const int64_t Q = a.gap_open, R = a.gap_extend;
     const int64_t L = 2 * Q + ((int64_t)a.m + n4) * R;
     const int64_t T = IMIN - Q - R - 1;
-    const int64_t U = (int64_t)min((int64_t)a.m, n4) * a.maxm;
+    int64_t U = (int64_t)min((int64_t)a.m, n4) * a.maxm;
+    // a lane the pair or int16 strip kernel scored exactly never held an H
+    // of 32767 or more: their admissibility bounds (engine.cpp nw_f16_limit,
+    // nw_int16_limit) cap every value of the matrix below it
+    if (w == 16 && a.nw_hmax16_ok && !long_lane) U = min(U, IMAX - 1);
     if (L >= T && U < IMAX && s > IMIN) return 0;
     return -1;
 }
@@ -99,7 +104,7 @@ __global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
     bool undecided = false;
     for (int b = 0; b < 2; b++) {
         if (!((a.widths >> b) & 1)) continue;
-        const int d = decide(a, b ? 16 : 8, s, len, gl < a.hmm_lanes ? a.hmm + gl : nullptr);
+        const int d = decide(a, b ? 16 : 8, s, len, gl < a.hmm_lanes ? a.hmm + gl : nullptr, gl < a.long_lanes);
         if (d < 0) undecided = true;
         else f |= (uint32_t)d << b;
     }

@@ -1161,13 +1161,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             // NW: the exact extremes of H the overflow counters decide from,
             // needed only when some long entry is too long for the bounds
             // (2Q + (m + n4)R below the flag threshold; counters.hip)
+            // (2Q + (m + n4)R below the flag threshold, or min(m, n4) maxM at
+            // I_MAX: the decide kernel's bounds, counters.hip)
             bool need_hmm = false;
             if (want_counts && nw) {
                 const int64_t n4max = (int64_t)D.group_ncols[0];
+                int64_t hi = maxM;                         // incl. the padding code 0 (as FlagArgs::maxm)
+                for (size_t i = 0; i < m; i++) hi = std::max(hi, M[qv.seq[i]]);
                 for (int b = 0; b < 2; b++) {
-                    const int64_t imin = b ? -32768 : -128;
-                    if (((bw == BIT_WIDTH_8) || b == 1) && 2 * (int64_t)Q + ((int64_t)m + n4max) * R < imin - Q - R - 1)
-                        need_hmm = true;
+                    const int64_t imin = b ? -32768 : -128, imax = b ? 32767 : 127;
+                    if ((bw == BIT_WIDTH_8) || b == 1)
+                        need_hmm = need_hmm || 2 * (int64_t)Q + ((int64_t)m + n4max) * R < imin - Q - R - 1 ||
+                                   std::min<int64_t>((int64_t)m, n4max) * std::max<int64_t>(hi, 0) >= imax;
                 }
             }
             if (need_hmm) {
@@ -1300,6 +1305,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 fa.hmm = D.d_hmm;
                 fa.hmm_lanes = long_groups * 64;
             }
+            fa.long_lanes = long_groups * 64;
+            // pair kernel (nw_f16_limit) and int16 strip kernel (nw_int16_limit):
+            // every H of an exactly scored lane stays below 32767
+            fa.nw_hmax16_ok = nw && (use_pair || !use_f16) && nmax16 > 0 ? 1 : 0;
             if (nw && D.ngroups > 0) {
                 // row-major NW replay: scratch for the longest entry's
                 // columns, 64..1024 lanes within 64 MiB

@@ -161,6 +161,8 @@ struct FlagArgs {
     // NW lanes [0, hmm_lanes) scored by long_kernel: exact (min, max) of H
     const int2* hmm;
     uint32_t hmm_lanes;
+    uint32_t long_lanes;       // lanes [0, long_lanes) were scored by long_kernel
+    int32_t nw_hmax16_ok;      // NW: the other lanes' kernel kept every H below 32767
 };
 hipError_t launch_flags(const FlagArgs& a, hipStream_t st);
 

@@ -1177,3 +1177,44 @@ def test_overflow_counters_long_nw_entries(qlen, waves, tmp_path):
     finally:
         S.set_option("long_waves", 0)
     S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("waves", [0, 1])
+def test_overflow_counters_nw_matrix_maximum(waves, tmp_path):
+    """NW whose matrix maximum reaches the 16-bit ceiling: a 2000-residue query
+    with constant scores +20/-5 against copies of itself (identity 60-100 %,
+    trimmed and extended) and random entries; the 16-bit flag then turns on
+    H == I_MAX somewhere inside the matrix, which the device takes from the
+    long kernel's exact extremes (the pair kernel's lanes cannot reach it);
+    widths 8 and 16 against the oracle's replays."""
+    rng = np.random.default_rng(77)
+    q = syn.protein_query(2000, 9)
+    seqs = []
+    for i in range(120):
+        if i % 6 == 0:
+            x = q.copy()
+            mut = rng.random(len(x)) < rng.uniform(0.0, 0.4)
+            x[mut] = rng.choice(syn.AA_CODES, int(mut.sum()))
+            a, b = int(rng.integers(0, 300)), int(rng.integers(1700, 2001))
+            x = np.concatenate([x[a:b], rng.choice(syn.AA_CODES, int(rng.integers(0, 800)))]).astype(np.uint8)
+            seqs.append(x)
+        else:
+            seqs.append(rng.choice(syn.AA_CODES, int(rng.integers(10, 3000))).astype(np.uint8))
+    db, off = po.pack_db(seqs)
+    configure(False, ("const", 20, -5), -10, -2)
+    S.init_db(_write_db(str(tmp_path), db, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    M = po.matrix_constant(20, -5)
+    flags = po.overflow_flags(1, q, db, off, M, -10, -2)
+    assert ((flags >> 1) & 1).sum() > 0                # the 16-bit flag occurs
+    exp_hits = po.search(1, q, seqs, M, -10, -2, 5)
+    S.set_option("long_waves", waves)
+    try:
+        for width in (S.BIT_WIDTH_8, S.BIT_WIDTH_16):
+            assert [(h["score"], h["id"]) for h in S.nw_align(qq, 5, width)] == exp_hits
+            st = S.stats()
+            o8, o16 = po.overflow_counts(width, flags)
+            assert (st["overflow_8"], st["overflow_16"]) == (o8 if width == 8 else 0, o16), width
+    finally:
+        S.set_option("long_waves", 0)
+    S.free_sequence(qq)
