@@ -89,49 +89,69 @@ __device__ __forceinline__ int decide(const FlagArgs& a, int w, int32_t s, uint3
     return -1;
 }
 
-__global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
-    const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
-    if (gl >= a.nlanes) return;
-    const uint32_t o = a.lane_out[gl];
-    if (o == 0xffffffffu) return;
-    const uint32_t len = a.lane_len[gl];
-    if (len == 0 || a.m == 0) {
-        a.flags[o] = 0;
-        return;
-    }
-    const int32_t s = a.scores[o];
-    uint32_t f = 0;
-    bool undecided = false;
-    for (int b = 0; b < 2; b++) {
-        if (!((a.widths >> b) & 1)) continue;
-        const int d = decide(a, b ? 16 : 8, s, len, gl < a.hmm_lanes ? a.hmm + gl : nullptr, gl < a.long_lanes);
-        if (d < 0) undecided = true;
-        else f |= (uint32_t)d << b;
-    }
-    if (undecided) {
-        // NW, ordinary penalties: which boundary chain first falls below the
-        // threshold T = I_MIN - Q - R - 1 -- the left one (H(i,-1) = Q + (i+1)R,
-        // met after ~4 i_L cells column by column) or the top one (H(-1,j) =
-        // Q + (j+1)R, met after ~j_T cells row by row); the flag is almost
-        // always decided where the first one crosses
-        bool rows = false;
-        if (a.nw && a.rlist && a.gap_extend < 0 && (a.ordinary & 2)) {
-            const int w = (a.widths & 1) ? 8 : 16;
-            const int64_t T = -(1ll << (w - 1)) - a.gap_open - a.gap_extend - 1;
-            const int64_t Rm = -(int64_t)a.gap_extend;
-            const int64_t cross = ((int64_t)a.gap_open - T) / Rm + 2;     // i_L ~ j_T
-            const int64_t n4 = (len + 3) & ~3u, full = (int64_t)a.m * n4;
-            const int64_t cost_col = a.m > cross ? 4 * cross : full;
-            const int64_t cost_row = n4 > cross && n4 <= a.rstride ? cross : full;
-            rows = cost_row * 16 < cost_col;
-        }
-        uint32_t* L = rows ? a.rlist : a.list;
-        const uint32_t i = atomicAdd(L, 1u);
-        L[1 + i] = gl;             // capacity: every lane
+// a lane's flags into the search's two counters (single view: FlagArgs::direct)
+__device__ __forceinline__ void count_direct(const FlagArgs& a, uint32_t f) {
+    unsigned long long c8 = 0, c16 = 0;
+    if (a.bw == 8) {
+        c8 = f & 1;
+        c16 = (f & 1) & (f >> 1);
     } else {
-        a.flags[o] = (uint8_t)f;
+        c16 = (f >> 1) & 1;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c8 += __shfl_xor(c8, o);
+        c16 += __shfl_xor(c16, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c8) atomicAdd(&a.direct[0], c8);
+        if (c16) atomicAdd(&a.direct[1], c16);
     }
 }
+
+__global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
+    const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t o = gl < a.nlanes ? a.lane_out[gl] : 0xffffffffu;
+    uint32_t f = 0;
+    bool undecided = false;
+    if (o != 0xffffffffu) {
+        const uint32_t len = a.lane_len[gl];
+        if (len > 0 && a.m > 0) {
+            const int32_t s = a.scores[o];
+            for (int b = 0; b < 2; b++) {
+                if (!((a.widths >> b) & 1)) continue;
+                const int d = decide(a, b ? 16 : 8, s, len, gl < a.hmm_lanes ? a.hmm + gl : nullptr,
+                                     gl < a.long_lanes);
+                if (d < 0) undecided = true;
+                else f |= (uint32_t)d << b;
+            }
+        }
+        if (undecided) {
+            // NW, ordinary penalties: which boundary chain first falls below the
+            // threshold T = I_MIN - Q - R - 1 -- the left one (H(i,-1) = Q + (i+1)R,
+            // met after ~4 i_L cells column by column) or the top one (H(-1,j) =
+            // Q + (j+1)R, met after ~j_T cells row by row); the flag is almost
+            // always decided where the first one crosses
+            bool rows = false;
+            if (a.nw && a.rlist && a.gap_extend < 0 && (a.ordinary & 2)) {
+                const int w = (a.widths & 1) ? 8 : 16;
+                const int64_t T = -(1ll << (w - 1)) - a.gap_open - a.gap_extend - 1;
+                const int64_t Rm = -(int64_t)a.gap_extend;
+                const int64_t cross = ((int64_t)a.gap_open - T) / Rm + 2;     // i_L ~ j_T
+                const int64_t n4 = (len + 3) & ~3u, full = (int64_t)a.m * n4;
+                const int64_t cost_col = a.m > cross ? 4 * cross : full;
+                const int64_t cost_row = n4 > cross && n4 <= a.rstride ? cross : full;
+                rows = cost_row * 16 < cost_col;
+            }
+            uint32_t* L = rows ? a.rlist : a.list;
+            const uint32_t i = atomicAdd(L, 1u);
+            L[1 + i] = gl;             // capacity: every lane
+        } else if (!a.direct) {
+            a.flags[o] = (uint8_t)f;
+        }
+    }
+    if (a.direct) count_direct(a, undecided ? 0u : f);     // (whole waves: the shuffles need every lane)
+}
+
 
 // The lane's residue at column j (compact code) and its matrix row; columns
 // past the end are the reference's code-0 padding.
@@ -314,7 +334,14 @@ __global__ void __launch_bounds__(64) flags_replay_rows_kernel(const FlagArgs a)
             if (!((a.widths >> b) & 1)) continue;
             f |= (uint32_t)replay_nw_rows(a, d, b ? 16 : 8, hep, a.rthreads) << b;
         }
-        a.flags[a.lane_out[gl]] = (uint8_t)f;
+        if (a.direct) {
+            const unsigned long long c8 = a.bw == 8 ? (f & 1) : 0;
+            const unsigned long long c16 = a.bw == 8 ? ((f & 1) & (f >> 1)) : ((f >> 1) & 1);
+            if (c8) atomicAdd(&a.direct[0], c8);
+            if (c16) atomicAdd(&a.direct[1], c16);
+        } else {
+            a.flags[a.lane_out[gl]] = (uint8_t)f;
+        }
     }
 }
 
@@ -333,7 +360,14 @@ __global__ void __launch_bounds__(64) flags_replay_kernel(const FlagArgs a) {
             const int x = a.nw ? replay_nw(a, d, w, hep, a.threads) : replay_sw(a, d, w, hep, a.threads);
             f |= (uint32_t)x << b;
         }
-        a.flags[a.lane_out[gl]] = (uint8_t)f;
+        if (a.direct) {
+            const unsigned long long c8 = a.bw == 8 ? (f & 1) : 0;
+            const unsigned long long c16 = a.bw == 8 ? ((f & 1) & (f >> 1)) : ((f >> 1) & 1);
+            if (c8) atomicAdd(&a.direct[0], c8);
+            if (c16) atomicAdd(&a.direct[1], c16);
+        } else {
+            a.flags[a.lane_out[gl]] = (uint8_t)f;
+        }
     }
 }
 
@@ -368,9 +402,11 @@ __global__ void __launch_bounds__(256) count_kernel(const CountArgs a) {
 
 hipError_t launch_flags(const FlagArgs& a, hipStream_t st) {
     if (a.nlanes == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(a.list, 0, 4, st);
-    if (e != hipSuccess) return e;
-    if (a.rlist && (e = hipMemsetAsync(a.rlist, 0, 4, st)) != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!a.lists_zeroed) {
+        if ((e = hipMemsetAsync(a.list, 0, 4, st)) != hipSuccess) return e;
+        if (a.rlist && (e = hipMemsetAsync(a.rlist, 0, 4, st)) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(flags_decide_kernel, dim3((a.nlanes + 255) / 256), dim3(256), 0, st, a);
     if (a.m > 0) hipLaunchKernelGGL(flags_replay_kernel, dim3(a.threads / 64), dim3(64), 0, st, a);
     if (a.m > 0 && a.rlist) hipLaunchKernelGGL(flags_replay_rows_kernel, dim3(a.rthreads / 64), dim3(64), 0, st, a);

@@ -1124,6 +1124,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (ind) w.zero = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
         else if (out.sparse && v + 1 == V) w.zero = D.d_fbuf;
         w.nzero = w.zero ? kFilterHeader : 0;
+        if (want_counts) {
+            // the overflow-flag replay lists start empty (flags pass below)
+            w.zero2[0] = D.d_flist;
+            w.zero2[1] = D.d_frlist;
+        }
 
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
@@ -1306,6 +1311,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 fa.hmm_lanes = long_groups * 64;
             }
             fa.long_lanes = long_groups * 64;
+            fa.bw = bw;
+            fa.lists_zeroed = 1;                       // by the wide kernel just before
+            // a single view (or a batch query): counted as decided, no flags
+            // array and no count pass
+            if (ind || V == 1) fa.direct = D.d_cnt + (ind ? 2 * v : 0);
             // pair kernel (nw_f16_limit) and int16 strip kernel (nw_int16_limit):
             // every H of an exactly scored lane stays below 32767
             fa.nw_hmax16_ok = nw && (use_pair || !use_f16) && nmax16 > 0 ? 1 : 0;
@@ -1325,19 +1335,19 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 fa.rwork = D.d_frwork;
             }
             check(launch_flags(fa, st), "overflow flags launch");
-            if (ind || v + 1 == V) {
-                // a batch query's own counters, or the search's over all views
+            if (!fa.direct && v + 1 == V) {
+                // the search's counters over all views
                 CountArgs ca{};
-                ca.flags = ind ? fa.flags : D.d_flags;
+                ca.flags = D.d_flags;
                 ca.entries = (uint32_t)E;
-                ca.views = ind ? 1u : (uint32_t)V;
+                ca.views = (uint32_t)V;
                 ca.bw = bw;
-                ca.out = D.d_cnt + (ind ? 2 * v : 0);
+                ca.out = D.d_cnt;
                 check(launch_count(ca, st), "overflow count launch");
-                if (v + 1 == V)
-                    check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st),
-                          "D2H counters");
-                counted = v + 1 == V;
+            }
+            if (v + 1 == V) {
+                check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st), "D2H counters");
+                counted = true;
             }
         }
         kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;

@@ -82,6 +82,7 @@ struct WideArgs {
     uint32_t ovf_cap;
     uint32_t* zero;            // nzero dwords cleared by block 0 (the next filter pass's counters)
     uint32_t nzero;
+    uint32_t* zero2[2];        // and these two dwords (the overflow-flag replay lists' counts), if set
 };
 
 // Device-side top-k candidate filter (single query view, k <= kFilterMaxK).
@@ -163,6 +164,12 @@ struct FlagArgs {
     uint32_t hmm_lanes;
     uint32_t long_lanes;       // lanes [0, long_lanes) were scored by long_kernel
     int32_t nw_hmax16_ok;      // NW: the other lanes' kernel kept every H below 32767
+    // single-view searches: the two counters are summed here directly (width
+    // 8: o8 += f8, o16 += f8 * f16; width 16: o16 += f16) and no count pass
+    // follows; null: flags only (multi-view, CountArgs)
+    unsigned long long* direct;
+    int32_t bw;
+    int32_t lists_zeroed;      // list counts were cleared by the wide kernel (WideArgs::zero2)
 };
 hipError_t launch_flags(const FlagArgs& a, hipStream_t st);
 

@@ -816,6 +816,7 @@ pair_kernel(const StripArgs a) {
 // recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
     if (blockIdx.x == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x >= 62 && a.zero2[threadIdx.x - 62]) *a.zero2[threadIdx.x - 62] = 0;
     const uint32_t n = min(*a.ovf_count, a.ovf_cap);
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
