@@ -108,13 +108,15 @@ __device__ __forceinline__ void count_direct(const FlagArgs& a, uint32_t f) {
     }
 }
 
+// one thread per entry (coalesced reads of the score and the entry's length
+// and lane)
 __global__ void __launch_bounds__(256) flags_decide_kernel(const FlagArgs a) {
-    const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t o = gl < a.nlanes ? a.lane_out[gl] : 0xffffffffu;
+    const uint32_t o = blockIdx.x * 256 + threadIdx.x;
     uint32_t f = 0;
     bool undecided = false;
-    if (o != 0xffffffffu) {
-        const uint32_t len = a.lane_len[gl];
+    if (o < a.entries) {
+        const uint2 ll = a.entry_lane[o];
+        const uint32_t len = ll.x, gl = ll.y;
         if (len > 0 && a.m > 0) {
             const int32_t s = a.scores[o];
             for (int b = 0; b < 2; b++) {
@@ -407,7 +409,7 @@ hipError_t launch_flags(const FlagArgs& a, hipStream_t st) {
         if ((e = hipMemsetAsync(a.list, 0, 4, st)) != hipSuccess) return e;
         if (a.rlist && (e = hipMemsetAsync(a.rlist, 0, 4, st)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(flags_decide_kernel, dim3((a.nlanes + 255) / 256), dim3(256), 0, st, a);
+    if (a.entries > 0) hipLaunchKernelGGL(flags_decide_kernel, dim3((a.entries + 255) / 256), dim3(256), 0, st, a);
     if (a.m > 0) hipLaunchKernelGGL(flags_replay_kernel, dim3(a.threads / 64), dim3(64), 0, st, a);
     if (a.m > 0 && a.rlist) hipLaunchKernelGGL(flags_replay_rows_kernel, dim3(a.rthreads / 64), dim3(64), 0, st, a);
     return hipGetLastError();

@@ -51,6 +51,8 @@ void DeviceDB::release() {
     d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
     dfree(d_hmm);
     d_hmm = nullptr;
+    dfree(d_entry_lane);
+    d_entry_lane = nullptr;
     hmm_cap = 0;
     d_res_cls = nullptr;
     cls_key.clear();
@@ -380,6 +382,20 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     check(hipMemcpy(D.d_res, H.res.data(), H.res.size(), hipMemcpyHostToDevice), "H2D residues");
     check(hipMemcpy(D.d_lane_len, H.lane_len.data(), H.lane_len.size() * 4, hipMemcpyHostToDevice), "H2D");
     check(hipMemcpy(D.d_lane_out, H.lane_out.data(), H.lane_out.size() * 4, hipMemcpyHostToDevice), "H2D");
+    {
+        // entry-ordered (length, lane): the overflow-flag pass reads them
+        // coalesced, entry by entry (lane order would gather the scores)
+        std::vector<uint32_t> el(std::max<size_t>(2 * E, 2), 0);
+        for (size_t l = 0; l < H.lane_out.size(); l++) {
+            const uint32_t e = H.lane_out[l];
+            if (e != 0xffffffffu) {
+                el[2 * (size_t)e] = H.lane_len[l];
+                el[2 * (size_t)e + 1] = (uint32_t)l;
+            }
+        }
+        dalloc((void**)&D.d_entry_lane, el.size() * 4, "entry lanes");
+        check(hipMemcpy(D.d_entry_lane, el.data(), el.size() * 4, hipMemcpyHostToDevice), "H2D");
+    }
     D.ngroups = (uint32_t)H.groups.size();
     D.group_ncols.resize(H.groups.size());
     D.ncols_sum = 0;
@@ -1289,6 +1305,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             fa.groups = D.d_groups;
             fa.lane_len = D.d_lane_len;
             fa.lane_out = D.d_lane_out;
+            fa.entry_lane = (const uint2*)D.d_entry_lane;
+            fa.entries = (uint32_t)E;
             fa.scores = a.scores;
             fa.query = D.d_query;
             fa.matrix = D.d_matrix;

@@ -88,6 +88,7 @@ struct DeviceDB {
     int32_t* d_frwork = nullptr;          // its scratch
     size_t frwork_cap = 0;                // int32 elements
     int2* d_hmm = nullptr;                // NW long entries: exact (min, max) of H per lane
+    uint32_t* d_entry_lane = nullptr;     // [entries] (length, lane) in entry order
     size_t hmm_cap = 0;                   // lanes
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
     unsigned long long* h_cnt = nullptr;  // pinned mirror

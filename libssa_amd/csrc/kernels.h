@@ -139,6 +139,8 @@ struct FlagArgs {
     const GroupDesc* groups;
     const uint32_t* lane_len;
     const uint32_t* lane_out;
+    const uint2* entry_lane;   // [entries] (length, lane) in entry order
+    uint32_t entries;
     const int32_t* scores;     // this view's exact scores (INT32_MIN: value elsewhere -> replay)
     const uint8_t* query;      // [m]
     const int64_t* matrix;     // [1024] compact code x query code
