@@ -82,6 +82,9 @@ def parse():
                         "(+X,B,Z,U,O), the reference generator's uniform 28 (generate_db.c:117-118)")
     p.add_argument("--lengths", default="gamma", choices=["gamma", "uniform"],
                    help="protein lengths: 1+Gamma(2,175) in [16,4096], or uniform [16,1000) like generate_db.c")
+    p.add_argument("--timeline", default=None,
+                   help="N=1: after the timed steps, one more step with the wave timeline on, saved "
+                        "to this .npy (tools/timeline.py analyses it)")
     p.add_argument("--torch-gather", action="store_true",
                    help="N>1: gather the shard logs with torch.distributed instead of ssa_amd_gather_logs")
     args = p.parse_args()
@@ -355,6 +358,12 @@ def main():
         replay_ms.append(st["replay_ms"])
     sync()
     elapsed = time.perf_counter() - t_start
+    if args.timeline and world == 1:
+        # untimed: every DP wave's start/end on the s_memrealtime clock
+        S.set_option("timeline", 1)
+        step()
+        np.save(args.timeline, S.timeline())
+        S.set_option("timeline", 0)
     if dist is not None:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)

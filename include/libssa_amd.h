@@ -86,8 +86,21 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        for the rest), always 4, always 1
  *   "long4_share_pct" P  auto: 4 waves per entry for groups longer than P % of
  *                        one SIMD's share of all columns
+ *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
+ *                        wave priority: none (default), one per SIMD, N
+ *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)
  * Unknown names print a warning. */
 void ssa_amd_set_option( const char * name, long value );
+
+/* The last search's wave timeline (option "timeline"; of the last query view
+ * for multi-view searches): rows of 4 uint32 --
+ *   pair_kernel: (group, start, end, place); long_kernel: (0x80000000 | lane
+ *   of its entry, start, end, place)
+ * start/end in s_memrealtime ticks (100 MHz, low 32 bits), place = XCC << 16 |
+ * HW_ID[15:0].  Rows never written stay zero.  Copies at most cap rows to out
+ * (may be NULL) and returns the row count.  A profiling aid (tools/timeline.py),
+ * not part of the reference's interface. */
+size_t ssa_amd_get_timeline( uint32_t * out, size_t cap );
 
 /* Scores the open DB against the query.  mode: SSA_AMD_TOPK or SSA_AMD_LOG.
  * Returns the number of hits written (at most cap; the log never exceeds

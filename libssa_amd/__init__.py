@@ -82,7 +82,7 @@ EXPORTS = {
                       "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
                       "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch",
                       "ssa_amd_dist_unique_id", "ssa_amd_dist_unique_id_bytes", "ssa_amd_dist_init",
-                      "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs"],
+                      "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs", "ssa_amd_get_timeline"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -128,6 +128,7 @@ def load():
         "ssa_amd_gather_logs": ([POINTER(ssa_hit_t), c_size_t, c_size_t, POINTER(ssa_hit_t)], c_size_t),
         "ssa_amd_merge_logs": ([POINTER(ssa_hit_t), POINTER(c_size_t), c_size_t, c_size_t, c_size_t,
                                 POINTER(ssa_hit_t)], c_size_t),
+        "ssa_amd_get_timeline": ([c_void_p, c_size_t], c_size_t),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -235,6 +236,19 @@ def stats():
     d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
     d["kernel"] = d["kernel"].decode()
     return d
+
+
+def timeline():
+    """ssa_amd_get_timeline: the last search's DP wave rows (option
+    "timeline") as a uint32 array [rows, 4]: (group or 0x80000000 | lane,
+    start, end, place), s_memrealtime ticks (100 MHz)."""
+    import numpy as np
+    L = load()
+    n = L.ssa_amd_get_timeline(None, 0)
+    out = np.zeros((n, 4), np.uint32)
+    if n:
+        L.ssa_amd_get_timeline(out.ctypes.data, n)
+    return out
 
 
 _hitbuf = [None, 0]     # reused output array (a fresh 64 Ki-entry ctypes array per call costs ~0.2 ms)

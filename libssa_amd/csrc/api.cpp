@@ -342,6 +342,17 @@ int ssa_amd_prepare_db(void) {
     return 0;
 }
 
+size_t ssa_amd_get_timeline(uint32_t* out, size_t cap) {
+    DeviceDB& D = device_db(0);
+    if (!D.d_timeline || D.timeline_rows == 0) return 0;
+    const size_t n = std::min(cap, D.timeline_rows);
+    if (out && n) {
+        check(hipSetDevice(D.device), "hipSetDevice");
+        check(hipMemcpy(out, D.d_timeline, n * sizeof(uint4), hipMemcpyDeviceToHost), "timeline copy");
+    }
+    return D.timeline_rows;
+}
+
 void ssa_amd_get_stats(ssa_amd_stats_t* out) {
     if (out) *out = stats();
 }
@@ -400,6 +411,8 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "long_share_pct")) cfg().long_share_pct = (int)value;
     else if (!strcmp(name, "long_waves")) cfg().long_waves = (int)value;
     else if (!strcmp(name, "long4_share_pct")) cfg().long4_share_pct = (int)value;
+    else if (!strcmp(name, "pair_prio_groups")) cfg().pair_prio_groups = (int)value;
+    else if (!strcmp(name, "timeline")) cfg().timeline = (int)value;
     else print_warning("unknown option %s", name);
 }
 

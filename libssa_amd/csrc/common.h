@@ -40,7 +40,9 @@ struct Config {
     int long_groups = -1;                 // leading groups scored by long_kernel: -1 auto, 0 never, N forced
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
-    int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
+    int long4_share_pct = 400;
+    int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)
+    int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)            // auto: 4 waves for groups longer than this % of a SIMD's share
 };
 Config& cfg();
 

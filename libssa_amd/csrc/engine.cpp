@@ -51,6 +51,9 @@ void DeviceDB::release() {
     d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
     dfree(d_hmm);
     d_hmm = nullptr;
+    dfree(d_timeline);
+    d_timeline = nullptr;
+    timeline_cap = timeline_rows = 0;
     dfree(d_entry_lane);
     d_entry_lane = nullptr;
     hmm_cap = 0;
@@ -1151,6 +1154,20 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (nmax16 == 0) kname = "wide_i64";
         if (v == 0) prep = now_ms() - t_prep0;
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
+        // option "timeline": one row per long_kernel lane and pair_kernel group
+        uint4* tl = nullptr;
+        D.timeline_rows = 0;
+        if (C.timeline && use_pair) {
+            const size_t rows = (size_t)long_groups * 64 + (D.ngroups - long_groups);
+            if (D.timeline_cap < rows) {
+                dfree(D.d_timeline);
+                check(hipMalloc((void**)&D.d_timeline, rows * sizeof(uint4)), "timeline");
+                D.timeline_cap = rows;
+            }
+            check(hipMemsetAsync(D.d_timeline, 0, rows * sizeof(uint4), st), "memset");
+            D.timeline_rows = rows;
+            tl = D.d_timeline;
+        }
         check(hipEventRecord(ev_k0, st), "event");
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
@@ -1223,6 +1240,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 la.scratch = D.d_lscratch;
             }
             la.gate = gate;
+            la.timeline = tl;
+            if (use_pair) la.lds_min = (uint32_t)pair_lds;
             gate_base = gate_total;
             if (long4 > 0) {
                 la.seq0 = 0;
@@ -1275,6 +1294,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             b.qpt_tail = D.d_qpt + tail_off;
             b.top = (const uint4*)D.d_top;
             b.g_first = long_groups;
+            b.timeline = tl ? tl + (size_t)long_groups * 64 : nullptr;
+            // the first wave on every SIMD holds one of the longest groups; it
+            // shares the SIMD with two other waves, so at equal priority it
+            // runs at a third of the issue rate and, on a DB that fills the chip
+            // only a few times over, outlasts the rest of the launch
+            {
+                const uint32_t pg = C.pair_prio_groups < 0 ? D.nsimd : (uint32_t)C.pair_prio_groups;
+                b.g_prio = (uint32_t)std::min<uint64_t>((uint64_t)long_groups + pg, D.ngroups);
+            }
             const int lnp = main_strips ? pnp : tail_np;
             check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {

@@ -88,6 +88,8 @@ struct DeviceDB {
     int32_t* d_frwork = nullptr;          // its scratch
     size_t frwork_cap = 0;                // int32 elements
     int2* d_hmm = nullptr;                // NW long entries: exact (min, max) of H per lane
+    uint4* d_timeline = nullptr;          // option "timeline": [long lanes][pair groups] wave rows
+    size_t timeline_cap = 0, timeline_rows = 0;
     uint32_t* d_entry_lane = nullptr;     // [entries] (length, lane) in entry order
     size_t hmm_cap = 0;                   // lanes
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]

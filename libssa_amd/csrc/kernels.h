@@ -40,6 +40,14 @@ struct StripArgs {
     const uint4* top;
     // pair_kernel: first group it scores (groups before it go to long_kernel)
     uint32_t g_first;
+    // pair_kernel: groups [g_first, g_prio) issue at raised wave priority --
+    // the longest groups, which set the launch's critical path when the DB
+    // fills the chip only a few times over (engine.cpp device_search)
+    uint32_t g_prio;
+    // wave timeline (option "timeline", ssa_amd_get_timeline): per pair-kernel
+    // group g - g_first, (g, start, end, place) -- s_memrealtime ticks
+    // (100 MHz) and (XCC << 16 | HW_ID & 0xffff); null: off
+    uint4* timeline;
 };
 
 // Long DB entries (long_kernel): the query rows split over the lanes of W
@@ -63,6 +71,12 @@ struct LongArgs {
                                // (the overflow counters' exact decision, counters.hip)
     uint32_t m, alpha;
     int32_t gap_open, gap_extend;
+    uint4* timeline;           // per entry s: (0x80000000 | s, start, end, place), like StripArgs
+    // dynamic LDS of a workgroup at least this: the concurrent pair kernel's
+    // (engine.cpp), so the hole a finished long workgroup leaves in a CU's
+    // LDS takes a pair workgroup (allocations are contiguous: a smaller hole
+    // beside the pair workgroups' would stay empty until one of those ends)
+    uint32_t lds_min;
 };
 constexpr int kLongWaves = 4;
 

@@ -493,6 +493,15 @@ constexpr int ad_ngroups(int np) { return ad_index(np - 1, np) + 1; }
 constexpr int pair_waves(int, bool) { return kPairWaves; }
 constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : 3; }
 
+// where a wave runs, for the timeline: XCC << 16 | HW_ID[15:0] (wave slot,
+// SIMD, pipe, CU, shader array, SE)
+__device__ inline uint32_t hw_place() {
+    uint32_t id, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return (xcc & 0xffu) << 16 | (id & 0xffffu);
+}
+
 template <int NP, bool NW, int NPT>
 __global__ void __launch_bounds__(64 * pair_waves(NP, NW), pair_occupancy(NP, NW))
 pair_kernel(const StripArgs a) {
@@ -503,6 +512,8 @@ pair_kernel(const StripArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t g = a.g_first + blockIdx.x * W + wave;
     const bool active = g < a.ngroups;
+    if (g < a.g_prio) __builtin_amdgcn_s_setprio(2);
+    const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     const uint32_t gg = active ? g : a.g_first;
 
     const GroupDesc gd = a.groups[gg];
@@ -785,6 +796,8 @@ pair_kernel(const StripArgs a) {
         strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, a.qpt_tail);
 
     if (!active) return;
+    if (a.timeline && lane == 0)
+        a.timeline[g - a.g_first] = make_uint4(g, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
     const uint32_t o = a.lane_out[gl];
     if (o == 0xffffffffu) return;
     if (len == 0) {
@@ -1146,6 +1159,10 @@ struct ProfSlice {
 template <int W, int RL, bool NW, bool TRK>
 __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a) {
     static_assert(!TRK || NW, "extremes are an NW counter input");
+    // at least the pair kernel's 168 VGPRs (kernel descriptor), for the same
+    // reason as LongArgs::lds_min: a finished long wave's registers must take
+    // a pair wave
+    asm volatile("" ::: "v167");
     extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][RP] profile of the pass
     __shared__ int2 ring[W > 1 ? W - 1 : 1][W > 1 ? kLongRing : 1];
     __shared__ int32_t wmax[kLongWaves], wlo[kLongWaves];
@@ -1156,6 +1173,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     // these waves are the launch's critical path: they issue before the
     // pair kernel's waves sharing their SIMD
     __builtin_amdgcn_s_setprio(3);
+    const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     if (a.gate && threadIdx.x == 0)
         __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = threadIdx.x & 63;
@@ -1475,6 +1493,8 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
             }
         }
     }
+    if (a.timeline && active && wr == 0 && lane == 0)
+        a.timeline[ss] = make_uint4(0x80000000u | ss, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
 }
 
 #undef LONG_ISSUE
@@ -1484,12 +1504,16 @@ size_t long_lds_bytes(uint32_t alpha, int w, int rl) { return (size_t)(alpha + 1
 template <int W, int RL, bool NW, bool TRK>
 static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW, TRK>, attr, (int)long_lds_bytes(32, W, RL));
+    // (the attribute leaves room for the kernel's static LDS: ring, maxima)
+    constexpr size_t kDynMax = kPairLdsMax - 8192;
+    const size_t need = long_lds_bytes(a.alpha, W, RL);
+    if (need > kDynMax) return hipErrorInvalidValue;
+    const size_t bytes = std::max<size_t>(need, std::min<size_t>(a.lds_min, kDynMax));
+    const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW, TRK>, attr, (int)kDynMax);
     if (e != hipSuccess) return e;
     constexpr int EPW = kLongWaves / W;
     const uint32_t blocks = (a.nseq + EPW - 1) / EPW;
-    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(blocks), dim3(64 * kLongWaves),
-                       long_lds_bytes(a.alpha, W, RL), st, a);
+    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
     return hipGetLastError();
 }
 

@@ -274,6 +274,45 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None):
         S.free_sequence(qq)
 
 
+def test_wave_timeline_and_priority_keep_scores():
+    """Options that only change scheduling -- the wave timeline (one row per
+    long_kernel lane and pair_kernel group, ssa_amd_get_timeline) and the raised
+    priority of the longest pair groups -- leave every score as the oracle's;
+    the timeline has a well-formed row for every group and long entry."""
+    rng = np.random.default_rng(5)
+    q = syn.protein_query(300, 55)
+    lens = np.array([3000, 2800, 2600] + list(rng.integers(1, 500, 2000)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    exp = po.scores(S.SW, q, codes, off, M, -11, -1)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            for lg, prio in ((1, -1), (0, 0), (2, 5)):
+                S.set_option("long_groups", lg)
+                S.set_option("pair_prio_groups", prio)
+                S.set_option("timeline", 1)
+                sc, ids = _full_scores(qq, S.SW, len(lens))
+                assert (sc == exp).all(), (lg, prio, np.nonzero(sc != exp)[0][:10])
+                t = S.timeline()
+                ngroups = (len(lens) + 63) // 64
+                assert t.shape == (lg * 64 + ngroups - lg, 4)
+                lng, pr = t[:lg * 64], t[lg * 64:]
+                assert (pr[:, 0] == np.arange(lg, ngroups)).all()
+                assert ((lng[:, 0] & 0x7fffffff) == np.arange(lg * 64)).all() and (lng[:, 0] >> 31 == 1).all()
+                dur = (t[:, 2].astype(np.int64) - t[:, 1].astype(np.int64)) % (1 << 32)
+                assert (dur < 100_000_000).all()          # under a second of the 100 MHz clock
+        finally:
+            S.set_option("timeline", 0)
+            S.set_option("long_groups", -1)
+            S.set_option("pair_prio_groups", 0)
+        S.free_sequence(qq)
+
+
 @pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 @pytest.mark.parametrize("waves", [4, 1])
