@@ -46,14 +46,19 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # pmc_c2_rel / pmc_c3_rel (48-row strips, diagonal-relative values),
 # pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals),
 # pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory),
-# pmc_{c2,c3,c5,ref}_r01g (+ diagonal add as v_add_u32, long_kernel: the
-# default, these values)
-VALU_INSTR_PER_CELL = {"strip16_sw": 5.59, "strip_f16m_sw": 4.79, "pair_f16_sw": 3.05, "pair_f16_nw": 2.74}
+# pmc_{c2,c3,c5,ref}_r01g (+ diagonal add as v_add_u32, long_kernel),
+# profiles/r02/pmc_c2_final (48-row SW strips, the default) and
+# profiles/r02/pmc_c3_np40 (80-row NW strips, the default).  Keyed by
+# (kernel, pair strip rows): the instruction count per cell depends on the
+# strip height.
+VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 3.04,
+                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.66}
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
 # profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
-# (tools/hotloop.py: per 48-row column SW 49 of 142.8, NW 49 of 128.8)
-VALU_FAST_SHARE = {"pair_f16_sw": 0.343, "pair_f16_nw": 0.380}
+# (tools/hotloop.py: per 48-row column SW 49 of 142.8, NW 49 of 128.8; the
+# 80-row NW column's share scaled by the census ratio at 48 rows)
+VALU_FAST_SHARE = {("pair_f16_sw", 48): 0.343, ("pair_f16_nw", 48): 0.380, ("pair_f16_nw", 80): 0.387}
 
 
 def parse():
@@ -75,7 +80,8 @@ def parse():
     p.add_argument("--long-tail", type=int, default=0,
                    help="replace N DB sequences by 5k-35k-residue ones (a UniProt-like length tail)")
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
-    p.add_argument("--pair-np", type=int, default=24, help="pair kernel main strip: 24 (48 rows) or 16 (32 rows)")
+    p.add_argument("--pair-np", type=int, default=0,
+                   help="pair kernel main strip of 2 x N rows: 0 auto (library's choice), 16, 24, 32, 36 (SW), 40")
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
     p.add_argument("--alphabet", default="bg20", choices=["bg20", "sprot25", "uniform28"],
                    help="protein residue set: 20 standard (BLOSUM62 background), Swiss-Prot-like 25 "
@@ -386,15 +392,16 @@ def main():
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
-        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_pair{args.pair_np}")
+        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_pair{st['strip_rows'] // 2}")
         if rec:
             traffic = rec["bytes_per_launch"]
     # VALU issue roofline: VOP3/VOP3P instructions issue at
     # 4.17 cycles per wave64 instruction per SIMD, v_add_u32 at 2.5 (measured
     # in isolation: profiles/r01/ubench_valu_rates4.txt); instructions per
     # cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01g).
-    instr_per_cell = VALU_INSTR_PER_CELL.get(st["kernel"]) if args.strip_np == 16 and args.pair_np == 24 else None
-    fast = VALU_FAST_SHARE.get(st["kernel"], 0.0)
+    kkey = (st["kernel"], st["strip_rows"])
+    instr_per_cell = VALU_INSTR_PER_CELL.get(kkey) if args.strip_np == 16 else None
+    fast = VALU_FAST_SHARE.get(kkey, 0.0)
     issue_cycles = (1.0 - fast) * 4.17 + fast * 2.5
     valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
@@ -414,7 +421,7 @@ def main():
                                f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
                                f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
                    "db_seqs_per_gpu": args.seqs, "db_total_seqs": db_total, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
-                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_np": args.pair_np, "strip_np": args.strip_np,
+                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_strip_rows": st["strip_rows"], "strip_np": args.strip_np,
                    "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

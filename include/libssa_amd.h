@@ -55,6 +55,8 @@ typedef struct {
     double prep_ms;          /* host work before the first kernel launch (profiles, uploads) */
     double upload_ms;        /* device time of the per-search uploads before the first kernel */
     double sync_wait_ms;     /* host time blocked in the final stream synchronisation */
+    uint32_t strip_rows;     /* pair kernel: rows of its main strips (2 x "pair_np"); 0: other kernels */
+    uint32_t reserved;
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -75,7 +77,9 @@ int ssa_amd_prepare_db( void );            /* pack + upload the DB now; returns 
 void ssa_amd_get_stats( ssa_amd_stats_t * out );
 /* Tuning knobs (results never change, only which kernel computes them):
  *   "strip_np" 8|16|32   int16 strip kernels: packed rows per strip
- *   "pair_np" 16|24      pair kernel main strip (32 / 48 rows)
+ *   "pair_np" 0|16|24|32|36|40  pair kernel main strip of 2 x pair_np rows; 0 (default):
+ *                        SW 24, NW the tallest of 40/32/24 whose pair table lets
+ *                        two workgroups share a CU (36 is SW only)
  *   "sw_kernel" 0|1      1: int16 strip kernel instead of the pair kernel
  *   "force_wide" 0|1     1: every entry through the int64 kernel
  *   "no_filter" 0|1      1: copy every score back (no device top-k filter)

@@ -65,7 +65,7 @@ class ssa_amd_stats_t(Structure):
                 ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
                 ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64),
                 ("kernel", ctypes.c_char * 32), ("prep_ms", c_double), ("upload_ms", c_double),
-                ("sync_wait_ms", c_double)]
+                ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("reserved", c_uint32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24

@@ -105,6 +105,7 @@ void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPl
     S.kernel_launches = (uint32_t)(sc.empty() ? 0 : sc[0].views);
     S.device = plan.empty() ? -1 : plan[0].device;
     snprintf(S.kernel, sizeof S.kernel, "%s", sc.empty() ? "" : sc[0].kernel);
+    S.strip_rows = sc.empty() ? 0 : sc[0].strip_rows;
 }
 
 void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {

@@ -36,7 +36,7 @@ struct Config {
     int force_wide = 0;                   // 1: score everything with the int64 kernel
     int sw_kernel = 0;                    // 0: f16-pattern kernel when applicable, 1: int16 kernel
     int no_filter = 0;                    // 1: copy every score back (no device top-k filter)
-    int pair_np = 24;                     // pair kernel main strip: 24 (48 rows, default) or 16 (32 rows)
+    int pair_np = 0;                      // pair kernel main strip: 2 x pair_np rows; 0 auto (engine.cpp pair_strip_np)
     int long_groups = -1;                 // leading groups scored by long_kernel: -1 auto, 0 never, N forced
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1

@@ -691,6 +691,25 @@ static uint32_t sw_rel_limit(size_t m, int Q, int R, int64_t minM, int64_t maxM)
 // UINT32_MAX when `beyond` cannot be covered; 0 when the int32 bound of
 // long_kernel does not hold or the option is off.
 static constexpr uint32_t kLongMaxGroups = 256;
+// pair kernel main strip half-height: the option when it names an
+// instantiated one; else SW 24 (48 rows, three waves per SIMD) and NW the
+// tallest of 40/32/24 whose table (prow^2 x (np+4) dwords) lets two
+// workgroups share a CU.  At two waves per SIMD the kernel issues nearly as
+// fast as at three (the wave timeline of a 548 k DB whose CUs held two pair
+// workgroups beside a long one for a third of the launch: -1.5 % overall),
+// and NW's 80-row strips (fewer boundary rows, per-strip and per-column work
+// over more rows) gain more than that: C3 +5 %.  SW's taller strips carry
+// the anti-diagonal accumulators too and measured 1-3 % slower (C2, C5;
+// same box, alternating runs).
+static int pair_strip_np(int opt, bool nw, uint32_t prow) {
+    if (opt == 16 || opt == 24 || opt == 32 || opt == 40 || (opt == 36 && !nw)) return opt;
+    if (!nw) return 24;
+    auto tbl = [&](int np) { return (size_t)prow * prow * (np + 4) * 4; };
+    for (int np : {40, 32})
+        if (2 * tbl(np) <= kPairLdsMax) return np;
+    return 24;
+}
+
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM) {
     const Config& C = cfg();
     const uint32_t need = (uint32_t)((beyond + 63) / 64);
@@ -849,6 +868,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     uint64_t wide_total = 0;
     uint64_t kernel_bytes = 0;
     const char* kname = "";
+    uint32_t srows = 0;
 
     for (size_t v = 0; v < V; v++) {
         const QueryView& qv = views[v];
@@ -871,8 +891,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // 28-symbol DB: '-', U, O and X score alike against a standard-residue
         // query -> 25 classes, a 75.7 KiB table, two workgroups per CU instead
         // of none); the class-coded residues are cached per class map.
-        const int pnp_v = C.pair_np == 24 ? 24 : 16;
-        std::vector<uint8_t> cls_of, cls_rep;
+                std::vector<uint8_t> cls_of, cls_rep;
         {
             uint32_t qset = 0;
             for (size_t i = 0; i < m; i++) qset |= 1u << (qv.seq[i] & 31);
@@ -890,9 +909,13 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 cls_of[c] = (uint8_t)k;
             }
         }
+        // (workgroups per CU, strip height) of the pair kernel for a compact
+        // alphabet of a codes
         auto pair_wgs = [&](size_t a) {
-            const size_t b = (a + 1) * (a + 1) * (pnp_v + 4) * 4;
-            return b > kPairLdsMax ? (size_t)0 : std::min<size_t>(3, (160 * 1024) / b);
+            const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1);
+            const size_t b = (a + 1) * (a + 1) * (pn + 4) * 4;
+            const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
+            return std::make_pair(w, pn);
         };
         const bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
                              pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
@@ -936,7 +959,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
         const uint32_t prow = A + 1;
         // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
-        const int pnp = C.pair_np == 24 ? 24 : 16;
+        const int pnp = pair_strip_np(C.pair_np, nw, prow);
         const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
         // pair kernel (diagonal-relative f16 patterns): only when no more than
         // a handful of entries exceed its length bound (those are re-scored
@@ -1152,6 +1175,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
+        srows = use_pair ? 2 * (uint32_t)pnp : 0;
         if (v == 0) prep = now_ms() - t_prep0;
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         // option "timeline": one row per long_kernel lane and pair_kernel group
@@ -1516,6 +1540,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 o.dev_o16 = want_counts ? D.h_cnt[2 * vv + 1] : 0;
                 if (hf[3]) take_wide(vv, hf[3], o, 0);
                 o.kernel = kname;
+                o.strip_rows = srows;
             }
         } else if (out.sparse) {
             const uint32_t nc = D.h_fbuf[0];
@@ -1589,6 +1614,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.wide_count = wide_total;
     out.kernel_bytes = kernel_bytes;
     out.kernel = kname;
+    out.strip_rows = srows;
 }
 
 }  // namespace ssa

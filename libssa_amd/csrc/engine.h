@@ -153,6 +153,7 @@ struct SearchScores {
     double kernel_ms = 0, wide_ms = 0, d2h_ms = 0, prep_ms = 0, upload_ms = 0, sync_wait_ms = 0;
     uint64_t wide_count = 0, kernel_bytes = 0;
     const char* kernel = "";
+    uint32_t strip_rows = 0;             // pair kernel main strip height
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;

@@ -491,7 +491,7 @@ constexpr int ad_ngroups(int np) { return ad_index(np - 1, np) + 1; }
 // 63.5 KiB table allows two workgroups per CU, and at 3-4 waves/SIMD the
 // strip's state no longer fits the registers -- they spill in the DP loop.)
 constexpr int pair_waves(int, bool) { return kPairWaves; }
-constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : 3; }
+constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : (np <= 24 ? 3 : 2); }
 
 // where a wave runs, for the timeline: XCC << 16 | HW_ID[15:0] (wave slot,
 // SIMD, pipe, CU, shader array, SE)
@@ -1597,6 +1597,9 @@ hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_
     // NW scores come from the tail strip's capture
     if (nw && npt == 0) return hipErrorInvalidValue;
     if (np == 24) return nw ? launch_pair_np<24, true>(a, npt, lds_bytes, st) : launch_pair_np<24, false>(a, npt, lds_bytes, st);
+    if (np == 32) return nw ? launch_pair_np<32, true>(a, npt, lds_bytes, st) : launch_pair_np<32, false>(a, npt, lds_bytes, st);
+    if (np == 40) return nw ? launch_pair_np<40, true>(a, npt, lds_bytes, st) : launch_pair_np<40, false>(a, npt, lds_bytes, st);
+    if (np == 36 && !nw) return launch_pair_np<36, false>(a, npt, lds_bytes, st);
     if (np == 16) return nw ? launch_pair_np<16, true>(a, npt, lds_bytes, st) : launch_pair_np<16, false>(a, npt, lds_bytes, st);
     if (np == 8) return nw ? launch_pair_np<8, true>(a, npt, lds_bytes, st) : launch_pair_np<8, false>(a, npt, lds_bytes, st);
     return hipErrorInvalidValue;

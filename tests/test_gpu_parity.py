@@ -220,7 +220,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
             S.set_option("sw_kernel", swk)
             for np_ in (8, 16, 32):
                 S.set_option("strip_np", np_)
-                for pnp in ((8, 16, 24) if swk == 0 and np_ == 16 else (24,)):
+                for pnp in ((16, 24, 32, 36, 40, 0) if swk == 0 and np_ == 16 else (0,)):
                     S.set_option("pair_np", pnp)
                     sc, ids = _full_scores(qq, algo, len(keep))
                     assert (ids == keep).all()
@@ -230,7 +230,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
                         fn = S.sw_align if algo == S.SW else S.nw_align
                         got = [(h["score"], h["id"]) for h in fn(qq, k, 16)]
                         assert got == po.topk(exp, keep.astype(np.uint64), k)
-        S.set_option("pair_np", 24)
+        S.set_option("pair_np", 0)
         S.set_option("strip_np", 16)
         S.set_option("sw_kernel", 0)
         S.free_sequence(qq)
@@ -298,6 +298,10 @@ def test_wave_timeline_and_priority_keep_scores():
                 S.set_option("timeline", 1)
                 sc, ids = _full_scores(qq, S.SW, len(lens))
                 assert (sc == exp).all(), (lg, prio, np.nonzero(sc != exp)[0][:10])
+                # pair_np auto: 48-row SW strips, 80-row NW strips
+                assert S.stats()["strip_rows"] == 48
+                S.nw_align(qq, 5, 16)
+                assert S.stats()["strip_rows"] == 80
                 t = S.timeline()
                 ngroups = (len(lens) + 63) // 64
                 assert t.shape == (lg * 64 + ngroups - lg, 4)
@@ -1066,11 +1070,11 @@ def test_gap_penalty_edges_vs_oracle(gaps, algo):
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
-        for pnp in (16, 24):
+        for pnp in (16, 24, 32, 36, 40, 0):
             S.set_option("pair_np", pnp)
             sc, ids = _full_scores(qq, algo, len(keep))
             assert (sc == exp).all(), (pnp, np.nonzero(sc != exp)[0][:10])
-        S.set_option("pair_np", 24)
+        S.set_option("pair_np", 0)
         S.free_sequence(qq)
 
 
