@@ -93,6 +93,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
  *                        wave priority: none (default), one per SIMD, N
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)
+ *   "pair_ticket" 1|0    pair-kernel workgroups take the next groups in start order
+ *                        (an atomic ticket; default) or in blockIdx order
  * Unknown names print a warning. */
 void ssa_amd_set_option( const char * name, long value );
 

@@ -41,6 +41,7 @@ struct Config {
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
     int long4_share_pct = 400;
+    int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)            // auto: 4 waves for groups longer than this % of a SIMD's share
 };

@@ -1301,6 +1301,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
             ta.zero = ovf;
+            if (C.pair_ticket) ta.zero_ticket = gate + 1;
             if (long_groups > 0) {
                 // (at most the first 512 workgroups: more may not all fit the
                 // chip at once, and the rest follow the first in order)
@@ -1318,6 +1319,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             b.qpt_tail = D.d_qpt + tail_off;
             b.top = (const uint4*)D.d_top;
             b.g_first = long_groups;
+            if (C.pair_ticket) b.ticket = gate + 1;    // zeroed by the tables kernel just before
             b.timeline = tl ? tl + (size_t)long_groups * 64 : nullptr;
             // the first wave on every SIMD holds one of the longest groups; it
             // shares the SIMD with two other waves, so at equal priority it

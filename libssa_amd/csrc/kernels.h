@@ -48,6 +48,12 @@ struct StripArgs {
     // group g - g_first, (g, start, end, place) -- s_memrealtime ticks
     // (100 MHz) and (XCC << 16 | HW_ID & 0xffff); null: off
     uint4* timeline;
+    // pair_kernel: workgroup -> groups by a start-order ticket (an atomic
+    // counter the tables kernel zeroes) instead of blockIdx: the workgroups'
+    // XCD is fixed by blockIdx round robin, so with blockIdx order a slower
+    // XCD still gets an equal share; tickets hand the next-longest groups to
+    // whichever workgroup starts next on any XCD.  Null: blockIdx order.
+    uint32_t* ticket;
 };
 
 // Long DB entries (long_kernel): the query rows split over the lanes of W
@@ -230,6 +236,7 @@ struct TableArgs {
     // on the stream cannot fill the CUs before the long entries are placed
     const uint32_t* gate;
     uint32_t gate_target;
+    uint32_t* zero_ticket;     // StripArgs::ticket, cleared by thread 0 (may be null)
 };
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
 

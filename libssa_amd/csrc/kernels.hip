@@ -510,7 +510,16 @@ pair_kernel(const StripArgs a) {
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t g = a.g_first + blockIdx.x * W + wave;
+    uint32_t wg = blockIdx.x;
+    if (a.ticket) {
+        // (through the table's first LDS dword: the first strip's staging
+        // starts behind a barrier, after every wave has read it; a static
+        // __shared__ word would not fit beside a 160 KiB table)
+        if (threadIdx.x == 0) lds[0] = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        wg = __builtin_amdgcn_readfirstlane(lds[0]);
+    }
+    const uint32_t g = a.g_first + wg * W + wave;
     const bool active = g < a.ngroups;
     if (g < a.g_prio) __builtin_amdgcn_s_setprio(2);
     const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
@@ -1040,6 +1049,7 @@ __device__ __forceinline__ int32_t table_val(const TableArgs& a, uint32_t c, uin
 
 __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
     if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;
+    if (a.zero_ticket && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_ticket = 0;
     if (a.gate && blockIdx.x == 0 && threadIdx.x == 0) {
         // the long entries' workgroups (another stream) start first; bounded
         // at ~20 ms of the 100 MHz real-time counter, so a gate that is never
@@ -1076,7 +1086,13 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const uint32_t prow = a.alpha + 1;
     const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);
-    if (total == 0) return a.zero ? hipMemsetAsync(a.zero, 0, 4, st) : hipSuccess;
+    if (total == 0) {
+        if (a.zero_ticket) {
+            const hipError_t e = hipMemsetAsync(a.zero_ticket, 0, 4, st);
+            if (e != hipSuccess) return e;
+        }
+        return a.zero ? hipMemsetAsync(a.zero, 0, 4, st) : hipSuccess;
+    }
     const uint32_t blocks = (uint32_t)std::min<size_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(pair_tables_kernel, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
