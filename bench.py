@@ -325,10 +325,34 @@ def main():
     # RCCL gather (ssa_amd_gather_logs); the RCCL unique id travels over the
     # torch process group once
     native = world > 1 and backend == "nccl" and not args.torch_gather
+    gather_note = None
     if native:
-        obj = [S.dist_unique_id() if rank == 0 else None]
+        # every rank agrees on the path: a rank whose RCCL setup fails sends
+        # the whole job to the torch.distributed gather instead of leaving the
+        # others inside a collective
+        uid = None
+        if rank == 0:
+            try:
+                uid = S.dist_unique_id()
+            except RuntimeError as e:
+                gather_note = str(e)
+        obj = [uid]
         dist.broadcast_object_list(obj, src=0)
-        S.dist_init(rank, world, obj[0])
+        ok = 0
+        if obj[0] is not None:
+            try:
+                S.dist_init(rank, world, obj[0])
+                ok = 1
+            except RuntimeError as e:
+                gather_note = str(e)
+        import torch
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if ok:
+                S.dist_finalize()
+            native = False
+            gather_note = gather_note or "RCCL setup failed on another rank"
 
     def step():
         if world == 1:
@@ -348,6 +372,16 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    gather_checked = None
+    if native:
+        # untimed: the RCCL gather's top-k must equal the torch.distributed
+        # gather of the same logs (every rank joins both collectives)
+        from libssa_amd.dist import global_topk
+        log = S.search(qq, algo, args.k, args.width, S.LOG)
+        a = S.gather_logs(log, args.k)
+        b = global_topk(log, args.k, dist, rank, world, dev)
+        if rank == 0:
+            gather_checked = [tuple(map(int, x[:2])) for x in a] == [tuple(map(int, x[:2])) for x in b]
     sync()
     kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms, upload_ms, sync_ms = [], [], [], [], [], [], [], []
     t_start = time.perf_counter()
@@ -444,7 +478,10 @@ def main():
                   "pack_ms": round(st["pack_ms"], 1)},
         "top_hit": list(res[0]) if res else None,
         "gather": ("ssa_amd_gather_logs (RCCL)" if native else "torch.distributed") if world > 1 else None,
+        "gather_equals_torch_gather": gather_checked,
     }
+    if gather_note:
+        out["gather_note"] = gather_note
     # the same DB and query as a reference-pinned fixture: the step's top-k
     # against the reference's own (tests/golden/fullsize.json)
     fx = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json"))).get(args.config)
