@@ -652,15 +652,22 @@ pair_kernel(const StripArgs a) {
         for (int p = 0; p < PF; p++)
             qn[p] = (uint32_t)p >= nquads ? make_uint4(0, 0, 0, 0) : qsrc[(size_t)p * qstride];
         // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
-        uint32_t dprev = a.alpha;
+        // LDS byte offsets: the pair row (d_j, d_{j-1}) sits at
+        // d_j * pairB + d_{j-1} * rowB; the previous residue's term is kept
+        // pre-scaled, so a column's address is one 24-bit multiply-add (the
+        // 32-bit form compiled to v_mad_u64_u32 + v_mul_lo_u32 + a base add)
+        constexpr uint32_t rowB = ROWW * 4;
+        const uint32_t pairB = prow * rowB;
+        const char* ldsb = (const char*)lds;
+        uint32_t dprevB = a.alpha * rowB;
         // P: the current column's profile operands.  The next column's row
         // is loaded into P in place behind the row loop, four rows at a time
         // (no second buffer: the registers pay for the SW accumulators A)
         uint32_t P[NPS];
         {
             const uint32_t d0 = rnext.x & 0xffu;
-            load_row<NPS>(P, lds + (d0 * prow + dprev) * ROWW);
-            dprev = d0;
+            load_row<NPS>(P, (const uint32_t*)(ldsb + (__umul24(d0, pairB) + dprevB)));
+            dprevB = __umul24(d0, rowB);
         }
 
         for (uint32_t b = 0; b < nblk; b++) {
@@ -686,8 +693,8 @@ pair_kernel(const StripArgs a) {
                     {
                         const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
                                                    : (rnext.x & 0xffu);
-                        nrow = lds + (dn * prow + dprev) * ROWW;
-                        dprev = dn;
+                        nrow = (const uint32_t*)(ldsb + (__umul24(dn, pairB) + dprevB));
+                        dprevB = __umul24(dn, rowB);
                     }
                     const uint32_t rbv = qw[u];
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
