@@ -701,10 +701,17 @@ static constexpr uint32_t kLongMaxGroups = 256;
 // over more rows) gain more than that: C3 +5 %.  SW's taller strips carry
 // the anti-diagonal accumulators too and measured 1-3 % slower (C2, C5;
 // same box, alternating runs).
-static int pair_strip_np(int opt, bool nw, uint32_t prow) {
+static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
     if (opt == 16 || opt == 24 || opt == 32 || opt == 40 || (opt == 36 && !nw)) return opt;
-    if (!nw) return 24;
     auto tbl = [&](int np) { return (size_t)prow * prow * (np + 4) * 4; };
+    if (!nw) {
+        // short SW queries whose rows fill 32-row strips better than 48-row
+        // ones run at four waves per SIMD when four tables fit a CU
+        // (profiles/r02/short_query_np.txt: q = 30 +1.4 %, q = 64 +2.1 %;
+        // q = 100 is 5 % faster at 48 rows)
+        const bool short_q = m <= 32 || (m > 48 && m <= 64);
+        return short_q && 4 * tbl(16) <= kPairLdsMax ? 16 : 24;
+    }
     for (int np : {40, 32})
         if (2 * tbl(np) <= kPairLdsMax) return np;
     return 24;
@@ -912,7 +919,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // (workgroups per CU, strip height) of the pair kernel for a compact
         // alphabet of a codes
         auto pair_wgs = [&](size_t a) {
-            const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1);
+            const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1, m);
             const size_t b = (a + 1) * (a + 1) * (pn + 4) * 4;
             const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
             return std::make_pair(w, pn);
@@ -959,7 +966,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
         const uint32_t prow = A + 1;
         // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
-        const int pnp = pair_strip_np(C.pair_np, nw, prow);
+        const int pnp = pair_strip_np(C.pair_np, nw, prow, m);
         const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
         // pair kernel (diagonal-relative f16 patterns): only when no more than
         // a handful of entries exceed its length bound (those are re-scored

@@ -1261,3 +1261,30 @@ def test_overflow_counters_nw_matrix_maximum(waves, tmp_path):
     finally:
         S.set_option("long_waves", 0)
     S.free_sequence(qq)
+
+
+@pytest.mark.gpu
+def test_short_sw_queries_take_32_row_strips():
+    """Short SW queries whose rows fill 32-row strips better (q <= 32 and
+    48 < q <= 64) run the pair kernel's 32-row strips at four waves per SIMD
+    (engine.cpp pair_strip_np); every score stays the oracle's, and the other
+    lengths keep 48-row strips."""
+    rng = np.random.default_rng(11)
+    lens = np.array(list(rng.integers(1, 700, 3000)) + [0, 1, 15, 16, 17], dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    keep = np.nonzero(lens > 0)[0]
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        for m, rows in ((1, 32), (17, 32), (30, 32), (32, 32), (33, 48), (48, 48), (49, 32), (64, 32), (65, 48)):
+            q = syn.protein_query(m, 100 + m)
+            exp = po.scores(S.SW, q, codes, off, M, -11, -1)
+            qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+            sc, ids = _full_scores(qq, S.SW, len(keep))
+            assert (ids == keep).all(), m
+            assert (sc == exp[keep]).all(), (m, np.nonzero(sc != exp[keep])[0][:10])
+            assert S.stats()["strip_rows"] == rows, m
+            S.free_sequence(qq)
