@@ -712,6 +712,10 @@ static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
         const bool short_q = m <= 32 || (m > 48 && m <= 64);
         return short_q && 4 * tbl(16) <= kPairLdsMax ? 16 : 24;
     }
+    // an NW query of at most 48 rows runs only the capture strip: at three
+    // waves per SIMD rather than the 80-row strips' two (q = 30: +4.8 %,
+    // profiles/r02/short_query_np.txt)
+    if (m <= 48) return 24;
     for (int np : {40, 32})
         if (2 * tbl(np) <= kPairLdsMax) return np;
     return 24;

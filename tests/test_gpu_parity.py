@@ -1268,7 +1268,8 @@ def test_short_sw_queries_take_32_row_strips():
     """Short SW queries whose rows fill 32-row strips better (q <= 32 and
     48 < q <= 64) run the pair kernel's 32-row strips at four waves per SIMD
     (engine.cpp pair_strip_np); every score stays the oracle's, and the other
-    lengths keep 48-row strips."""
+    lengths keep 48-row strips; NW queries of up to 48 rows take 48-row
+    strips instead of 80-row ones."""
     rng = np.random.default_rng(11)
     lens = np.array(list(rng.integers(1, 700, 3000)) + [0, 1, 15, 16, 17], dtype=np.int64)
     off = np.zeros(len(lens) + 1, np.uint64)
@@ -1287,4 +1288,10 @@ def test_short_sw_queries_take_32_row_strips():
             assert (ids == keep).all(), m
             assert (sc == exp[keep]).all(), (m, np.nonzero(sc != exp[keep])[0][:10])
             assert S.stats()["strip_rows"] == rows, m
+            if m in (30, 48, 49, 65):
+                # NW: 48-row strips up to 48 query rows, then 80-row ones
+                exp_nw = po.scores(S.NW, q, codes, off, M, -11, -1)
+                sc, ids = _full_scores(qq, S.NW, len(keep))
+                assert (sc == exp_nw[keep]).all(), (m, np.nonzero(sc != exp_nw[keep])[0][:10])
+                assert S.stats()["strip_rows"] == (48 if m <= 48 else 80), m
             S.free_sequence(qq)
