@@ -4,6 +4,8 @@
 //   slow5:   pk_add, max3, pk_add, max3, max3  (all packed / VOP3)
 //   cur:     the SW/NW row today: pk_add, max3, add_u32, max3, max3
 //   fastadd: the diagonal add as v_add_u32 too: add, max3, add, max3, max3
+//   batch4:  the adds of two groups back to back: add x4, max3 x6
+//   pairs:   add, add, max3 x3
 //   fast5:   5 x v_add_u32
 // Build: hipcc --offload-arch=gfx950 -O3 -o mix_rates mix_rates.hip
 #include <hip/hip_runtime.h>
@@ -36,6 +38,8 @@
 KERNEL(k_slow5, PK("%0") MX("%1") PK("%2") MX("%3") MX("%4") PK("%5") MX("%6") PK("%7") MX("%8") MX("%9"))
 KERNEL(k_cur, PK("%0") MX("%1") AD("%2") MX("%3") MX("%4") PK("%5") MX("%6") AD("%7") MX("%8") MX("%9"))
 KERNEL(k_fastadd, AD("%0") MX("%1") AD("%2") MX("%3") MX("%4") AD("%5") MX("%6") AD("%7") MX("%8") MX("%9"))
+KERNEL(k_batch4, AD("%0") AD("%1") AD("%2") AD("%3") MX("%4") MX("%5") MX("%6") MX("%7") MX("%8") MX("%9"))
+KERNEL(k_pairs, AD("%0") AD("%1") MX("%2") MX("%3") MX("%4") AD("%5") AD("%6") MX("%7") MX("%8") MX("%9"))
 KERNEL(k_fast5, AD("%0") AD("%1") AD("%2") AD("%3") AD("%4") AD("%5") AD("%6") AD("%7") AD("%8") AD("%9"))
 
 template <typename K>
@@ -63,6 +67,8 @@ int main() {
     run("slow5", k_slow5);
     run("cur", k_cur);
     run("fastadd", k_fastadd);
+    run("batch4", k_batch4);
+    run("pairs", k_pairs);
     run("fast5", k_fast5);
     return 0;
 }
