@@ -287,6 +287,10 @@ FULLSIZE = {
                gap_open=-10, gap_extend=-2, algo="nw", width=16, alphabet="bg20"),
     "c4": dict(kind="protein", n=10_000_000, i1=1_250_000, seed=42, qlen=400, qseed=7, matrix="blosum62",
                gap_open=-11, gap_extend=-1, algo="sw", width=8, alphabet="bg20"),
+    # the whole 10 M C4 DB on one GPU (top-k and counters pinned; the GPU
+    # test does not pull the 10 M-entry log through Python)
+    "c4full": dict(kind="protein", n=10_000_000, i1=10_000_000, seed=42, qlen=400, qseed=7, matrix="blosum62",
+                   gap_open=-11, gap_extend=-1, algo="sw", width=8, alphabet="bg20"),
     "c5": dict(kind="dna", n=50_000_000, i1=1_000_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
                gap_open=-4, gap_extend=-2, algo="sw", width=16),
     "sp25": dict(kind="protein", n=500_000, i1=500_000, seed=44, qlen=400, qseed=7, matrix="blosum62",
