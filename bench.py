@@ -485,13 +485,16 @@ def main():
     # the same DB and query as a reference-pinned fixture: the step's top-k
     # against the reference's own (tests/golden/fullsize.json)
     fxs = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))
-    fx = fxs.get(args.config)
-    if fx and fx["i1"] != args.seqs:
-        fx = fxs.get(args.config + "full", fx)       # c4full: the whole 10 M DB
-    if (fx and world == 1 and args.long_tail == 0 and args.alphabet == fx.get("alphabet", "bg20")
-            and args.lengths == fx.get("lengths", "gamma") and fx["n"] == db_total and fx["i1"] == args.seqs
-            and fx["qlen"] == args.qlen and fx["algo"] == args.algo and fx["gap_open"] == args.gap_open
-            and fx["gap_extend"] == args.gap_extend and fx["matrix"] == args.matrix and args.k in (1, 10, 64)):
+
+    def same_db(fx):
+        return (fx.get("kind", "protein") == args.db and args.alphabet == fx.get("alphabet", "bg20")
+                and args.lengths == fx.get("lengths", "gamma") and fx["n"] == db_total and fx["i1"] == args.seqs
+                and fx["qlen"] == args.qlen and fx["algo"] == args.algo and fx["gap_open"] == args.gap_open
+                and fx["gap_extend"] == args.gap_extend and fx["matrix"] == args.matrix)
+    # the fixture of this exact DB and search, if any (c2, c3, the c4 / c5
+    # shares, c4full = the whole 10 M DB, c5share8 = one GPU's C5 share at N = 8)
+    fx = next((f for f in fxs.values() if same_db(f)), None)
+    if fx and world == 1 and args.long_tail == 0 and args.k in (1, 10, 64):
         out["topk_vs_reference"] = "match" if [list(x) for x in res] == fx[f"top{args.k}"] else "MISMATCH"
     if world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle as po

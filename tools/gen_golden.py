@@ -293,6 +293,9 @@ FULLSIZE = {
                    gap_open=-11, gap_extend=-1, algo="sw", width=8, alphabet="bg20"),
     "c5": dict(kind="dna", n=50_000_000, i1=1_000_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
                gap_open=-4, gap_extend=-2, algo="sw", width=16),
+    # one GPU's share of C5 at N = 8 (the first 6.25 M of the 50 M reads)
+    "c5share8": dict(kind="dna", n=50_000_000, i1=6_250_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
+                     gap_open=-4, gap_extend=-2, algo="sw", width=16),
     "sp25": dict(kind="protein", n=500_000, i1=500_000, seed=44, qlen=400, qseed=7, matrix="blosum62",
                  gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="sprot25"),
     "u28": dict(kind="protein", n=200_000, i1=200_000, seed=45, qlen=400, qseed=7, matrix="blosum62",
