@@ -293,6 +293,11 @@ FULLSIZE = {
                    gap_open=-11, gap_extend=-1, algo="sw", width=8, alphabet="bg20"),
     "c5": dict(kind="dna", n=50_000_000, i1=1_000_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
                gap_open=-4, gap_extend=-2, algo="sw", width=16),
+    # C2's weak-scaling DBs at N = 2, 4, 8 (N x 1 M sequences; rank r
+    # searches IDs [r M, (r+1) M)): the global top-k bench.py gathers at N > 1
+    **{f"c2x{w}": dict(kind="protein", n=w * 1_000_000, i1=w * 1_000_000, seed=42, qlen=400, qseed=7,
+                       matrix="blosum62", gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="bg20")
+       for w in (2, 4, 8)},
     # one GPU's share of C5 at N = 8 (the first 6.25 M of the 50 M reads)
     "c5share8": dict(kind="dna", n=50_000_000, i1=6_250_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
                      gap_open=-4, gap_extend=-2, algo="sw", width=16),
