@@ -1098,9 +1098,11 @@ def _fullsize_inputs(c):
 # fixtures pinned by top-k and counters only (the GPU test does not pull their
 # multi-million-entry logs through Python)
 LARGE = ("c4full", "c5share8")
+# C2's weak-scaling DBs (bench.py at N = 2/4/8): pinned through the shard path
+SHARDED = ("c2x2",)
 
 
-@pytest.mark.parametrize("name", sorted(k for k in FULL if k not in LARGE))
+@pytest.mark.parametrize("name", sorted(k for k in FULL if k not in LARGE and not k.startswith("c2x")))
 def test_fullsize_matches_reference_hash(name, tmp_path):
     """BASELINE.json's configurations at full size (C2, C3: 1 M sequences) or
     one GPU's share (C4: the first 1.25 M of the 10 M DB at width 8; C5: the
@@ -1176,6 +1178,41 @@ def test_large_db_matches_reference(name, tmp_path):
         st = S.stats()
         assert [st["overflow_8"], st["overflow_16"]] == c["overflow"], k
     S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("name", [k for k in SHARDED if k in FULL])
+def test_sharded_db_logs_merge_to_reference_topk(name, tmp_path):
+    """bench.py's multi-GPU path at full size, on one GPU: C2's 2 M-sequence
+    weak-scaling DB searched as its two 1 M ID shards (each packed with its
+    global ID offset, ssa_amd_set_id_offset), their insertion logs merged by
+    the native shard merge (ssa_amd_merge_logs, what ssa_amd_gather_logs
+    runs on rank 0): top-1/10/64 equal the reference's own search of the
+    whole DB (tests/golden/fullsize.json)."""
+    c = FULL[name]
+    world = c["n"] // 1_000_000
+    q = syn.protein_query(c["qlen"], c["qseed"])
+    configure(False, ("builtin", c["matrix"]), c["gap_open"], c["gap_extend"])
+    logs = []
+    try:
+        for r in range(world):
+            i0, i1 = r * 1_000_000, (r + 1) * 1_000_000
+            codes, off = syn.protein_db_range(c["n"], c["seed"], i0, i1, query=q, alphabet=c.get("alphabet", "bg20"),
+                                              lo=16, hi=4096)
+            path = os.path.join(str(tmp_path), f"db{r}.fas")
+            syn.write_fasta(path, codes, off, False)
+            del codes, off
+            S.init_db(path)
+            S.set_id_offset(i0)
+            S.prepare_db()
+            os.remove(path)
+            qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+            logs.append(S.search(qq, S.SW, 64, c["width"], S.LOG))
+            S.free_sequence(qq)
+    finally:
+        S.set_id_offset(0)
+    for k in (1, 10, 64):
+        got = [[int(a), int(b)] for a, b in S.merge_logs([[h for h in L] for L in logs], k)]
+        assert got == c[f"top{k}"], k
 
 
 @pytest.mark.parametrize("gaps", [(-11, 2), (3, -1)])
