@@ -14,6 +14,18 @@ log, the logs are gathered to rank 0 over RCCL and replayed there
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|ref] [--seqs S]
 
+Launch: under torchrun (WORLD_SIZE set) every process is one rank.  Without
+it, `--gpus N` with N > 1 makes this process a launcher that never imports
+torch or touches a GPU: it starts N child processes of bench.py (RANK,
+LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), waits for them,
+prints rank 0's JSON line and exits non-zero when any rank fails (the
+reference fans out and joins its workers inside one call,
+src/util/thread_pool.c:76-86, src/algo/manager.c:141-145).  N larger than
+the visible GPU count is refused, except as a gloo rehearsal
+(SSA_DIST_BACKEND=gloo: several ranks share a GPU, the exchange goes over
+gloo).  --launch-selftest runs only the launch (ranks, env, rendezvous,
+failure propagation) without the library.
+
 Other BASELINE.json configurations (parity/extra measurements; the default
 line is C2): --config c3 = NW BLOSUM50 -10/-2, 1000-residue query, 1 M
 sequences per GPU; c4 = SW BLOSUM62 -11/-1 (API width 8) over 10 M sequences
@@ -77,13 +89,13 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--long-tail", type=int, default=0,
+    p.add_argument("--long-tail", type=int, default=None,
                    help="replace N DB sequences by 5k-35k-residue ones (a UniProt-like length tail)")
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
     p.add_argument("--pair-np", type=int, default=0,
                    help="pair kernel main strip of 2 x N rows: 0 auto (library's choice), 16, 24, 32, 36 (SW), 40")
     p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
-    p.add_argument("--alphabet", default="bg20", choices=["bg20", "sprot25", "uniform28"],
+    p.add_argument("--alphabet", default=None, choices=["bg20", "sprot25", "uniform28"],
                    help="protein residue set: 20 standard (BLOSUM62 background), Swiss-Prot-like 25 "
                         "(+X,B,Z,U,O), the reference generator's uniform 28 (generate_db.c:117-118)")
     p.add_argument("--lengths", default="gamma", choices=["gamma", "uniform"],
@@ -93,12 +105,20 @@ def parse():
                         "to this .npy (tools/timeline.py analyses it)")
     p.add_argument("--torch-gather", action="store_true",
                    help="N>1: gather the shard logs with torch.distributed instead of ssa_amd_gather_logs")
+    p.add_argument("--launch-selftest", action="store_true",
+                   help="N>1 launcher check: the ranks verify their env and meet over gloo, no library/GPU")
+    p.add_argument("--selftest-fail-rank", type=int, default=-1,
+                   help="--launch-selftest: this rank exits with status 3 before the rendezvous")
     args = p.parse_args()
     cfg = CONFIGS[args.config]
     for key in ("qlen", "algo", "matrix", "gap_open", "gap_extend"):
         if getattr(args, key) is None:
             setattr(args, key, cfg[key])
     args.db = cfg["db"]
+    if args.alphabet is None:
+        args.alphabet = cfg.get("alphabet", "bg20")
+    if args.long_tail is None:
+        args.long_tail = cfg.get("long_tail", 0)
     args.width = cfg["width"]
     args.strong = cfg["total_seqs"] is not None
     return args
@@ -120,6 +140,13 @@ CONFIGS = {
     # on a synthetic DB of that sequence count (no network for Swiss-Prot)
     "ref": dict(algo="sw", matrix="blosum50", gap_open=-3, gap_extend=-1, qlen=513, db="protein",
                 seqs=548_208, total_seqs=None, width=16, query_file="tests/golden/data/P18080.fasta"),
+    # the same in Swiss-Prot's form: its 25-symbol alphabet (+X, B, Z, U, O,
+    # util_sequence.c:36-44) and a length tail of 300 entries of 5-35 k
+    # residues (UniProt holds entries up to ~35 k); tests/golden/fullsize.json
+    # "sprot" pins it to the reference's own search
+    "sprot": dict(algo="sw", matrix="blosum50", gap_open=-3, gap_extend=-1, qlen=513, db="protein",
+                  seqs=548_208, total_seqs=None, width=16, query_file="tests/golden/data/P18080.fasta",
+                  alphabet="sprot25", long_tail=300),
 }
 
 
@@ -214,51 +241,196 @@ def cpu_baseline(codes, off, q, M, args):
             "host_share": share, "sample": f"first {sample} DB sequences, oracle int64 scalar port on {cores} threads"}
 
 
+def visible_gpus():
+    """GPUs a child process would see, counted in a throwaway subprocess
+    (torch.cuda.device_count() does not initialise HIP on this image, and the
+    launcher itself never imports torch)."""
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return 0
+
+
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch(args, argv):
+    """Parent of an N-rank run started as `bench.py --gpus N` (no WORLD_SIZE):
+    spawns the ranks, forwards their output, re-prints rank 0's JSON line,
+    and propagates the first failure (the other ranks are stopped)."""
+    import signal
+    import threading
+    N = args.gpus
+    backend = os.environ.get("SSA_DIST_BACKEND", "nccl")
+    ngpu = None
+    if not args.launch_selftest:
+        ngpu = visible_gpus()
+        if N > ngpu and backend != "gloo":
+            print(f"bench.py: --gpus {N} requested but {ngpu} GPU(s) visible; refusing to double ranks up "
+                  f"(a gloo rehearsal on fewer GPUs: SSA_DIST_BACKEND=gloo)", file=sys.stderr)
+            return 2
+        if ngpu < 1:
+            print("bench.py: no GPU visible", file=sys.stderr)
+            return 2
+    port = free_port()
+    procs = []
+    lines = []
+    me = os.path.abspath(__file__)
+    for r in range(N):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(N), LOCAL_WORLD_SIZE=str(N),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SSA_BENCH_LAUNCHER="bench.py --gpus")
+        if ngpu is not None:
+            env["SSA_BENCH_VISIBLE_GPUS"] = str(ngpu)
+        procs.append(subprocess.Popen([sys.executable, "-u", me, *argv],
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), env=env))
+
+    def pump():
+        # rank 0's stdout: progress lines through, the JSON line held back
+        for raw in procs[0].stdout:
+            line = raw.decode(errors="replace").rstrip("\n")
+            if line.startswith("{"):
+                lines.append(line)
+            else:
+                print(line, flush=True)
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad[0]
+            print(f"bench.py: rank {failed[0]} exited with status {failed[1]}; stopping the other ranks",
+                  file=sys.stderr, flush=True)
+            deadline = time.time() + 10
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+            deadline = time.time() + 10
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.2)
+    th.join(10)
+    if failed is not None:
+        return failed[1] if failed[1] > 0 else 1
+    if not lines:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+def launch_selftest(args):
+    """A rank of `bench.py --gpus N --launch-selftest`: checks the launch
+    environment and meets the other ranks over gloo (no library, no GPU)."""
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ["LOCAL_RANK"])
+    assert world == args.gpus and 0 <= rank < world and local == rank, (rank, local, world, args.gpus)
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1" and int(os.environ["MASTER_PORT"]) > 0
+    if rank == args.selftest_fail_rank:
+        print(f"rank {rank}: failing on purpose (--selftest-fail-rank)", file=sys.stderr, flush=True)
+        sys.exit(3)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "local_rank": local, "pid": os.getpid(),
+                                 "launcher": os.environ.get("SSA_BENCH_LAUNCHER")})
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_selftest": "ok", "world": world, "ranks": got}), flush=True)
+    dist.destroy_process_group()
+
+
 def make_shard(args, cfg, rank, world):
     """This rank's contiguous ID slice of the config's synthetic DB, from the
     block-seeded generators (libssa_amd/synthetic.py: a slice is
     byte-identical to the same IDs of the whole DB).  Weak configs (C2/C3/ref):
-    an N x seqs DB, 1 M per rank; strong ones (C4/C5): the fixed 10 M / 50 M DB
-    cut into N ID ranges, so every N searches the same DB.  At N = 1 C2 and C3
-    are exactly tests/golden/fullsize.json's c2/c3 DBs.
+    an N x seqs DB, ~1 M per rank; strong ones (C4/C5): the fixed 10 M / 50 M
+    DB, so every N searches the same DB.  At N > 1 the ranks' ranges are cut
+    so that their residue sums balance (ssa_amd_shard_bounds),
+    not by sequence count.  At N = 1 C2 and C3 are exactly
+    tests/golden/fullsize.json's c2/c3 DBs.
     --seqs: the per-rank sequence count of a weak config's DB, or the per-rank
-    share of a strong config's fixed DB.
-    Returns (query, codes, offsets, first global ID, DB size)."""
+    share of a strong config's fixed DB (then cut by count: the first share is
+    the c4/c5 fixtures' DB).
+    Returns (query, codes, offsets, first global ID, DB size, IDs the job searches)."""
+    import libssa_amd as S
     from libssa_amd import synthetic as syn
+    dna = args.db == "dna"
+    if dna:
+        q = syn.dna_query(args.qlen, 8)
+    else:
+        q = read_query_file(cfg["query_file"]) if cfg.get("query_file") else syn.protein_query(args.qlen, 7)
+    hi = 4096 if args.lengths == "gamma" else 1000
     if cfg["total_seqs"] is None:
         per = args.seqs if args.seqs is not None else cfg["seqs"]
-        total = per * world
+        total = job = per * world
+        balanced = world > 1
     else:
-        # strong: --seqs is this rank's share of the fixed DB (C4: the first
-        # 1.25 M of the 10 M DB at N = 1 is the c4 fixture's share)
         total = cfg["total_seqs"]
         per = args.seqs if args.seqs is not None else (total + world - 1) // world
-    i0 = min(total, rank * per)
-    i1 = min(total, i0 + per)
-    if args.db == "dna":
-        q = syn.dna_query(args.qlen, 8)
+        job = min(total, per * world)
+        balanced = world > 1 and args.seqs is None
+    if balanced and not dna:
+        lens = syn.protein_lengths_range(total, 42, 0, job, query=q, lo=16, hi=hi, lengths=args.lengths)
+        b = S.shard_bounds(lens, world)
+        i0, i1 = b[rank], b[rank + 1]
+    else:
+        # equal-length reads (C5), or one GPU: cutting by count is balanced
+        i0 = min(job, rank * per)
+        i1 = min(job, i0 + per) if rank + 1 < world else job
+    if dna:
         codes, off = syn.dna_reads_range(total, 43, i0, i1, 150, query=q)
-        return q, codes, off, i0, total
-    q = read_query_file(cfg["query_file"]) if cfg.get("query_file") else syn.protein_query(args.qlen, 7)
+        return q, codes, off, i0, total, job
     codes, off = syn.protein_db_range(total, 42, i0, i1, query=q, alphabet=args.alphabet, lengths=args.lengths,
-                                      lo=16, hi=4096 if args.lengths == "gamma" else 1000)
-    return q, codes, off, i0, total
+                                      lo=16, hi=hi)
+    return q, codes, off, i0, total, job
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the launcher: no torch, no GPU in this process
+        sys.exit(launch(args, sys.argv[1:]))
+    if args.launch_selftest:
+        if "WORLD_SIZE" in os.environ:
+            launch_selftest(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch
-        local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks on one GPU
     dist = None
     backend = os.environ.get("SSA_DIST_BACKEND", "nccl")   # nccl == RCCL on ROCm; gloo for rehearsal
     dev = "cuda" if backend == "nccl" else "cpu"
+    ranks_per_gpu = 1
     if world > 1:
         import torch
         import torch.distributed as dist
+        ngpu = torch.cuda.device_count()
+        if local >= ngpu:
+            if backend != "gloo":
+                raise SystemExit(f"bench.py rank {rank}: LOCAL_RANK {local} but only {ngpu} GPU(s) visible")
+            # gloo rehearsal: several ranks share a GPU
+            ranks_per_gpu = -(-world // max(1, ngpu))
+            local = local % max(1, ngpu)
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
 
@@ -286,27 +458,13 @@ def main():
 
     # --- synthetic shard (untimed): generate, write FASTA, pack into HBM
     t0 = time.time()
-    q, codes, off, id0, db_total = make_shard(args, cfg, rank, world)
+    q, codes, off, id0, db_total, job_ids = make_shard(args, cfg, rank, world)
     args.qlen = len(q)
     args.seqs = len(off) - 1
-    if not dna:
-        if args.long_tail > 0:
-            # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
-            # residues); the others keep theirs
-            rng = np.random.default_rng(77 + rank)
-            lens = np.diff(off).astype(np.int64)
-            tail = np.zeros(args.seqs, bool)
-            tail[np.arange(args.long_tail) * (args.seqs // args.long_tail)] = True
-            lens[tail] = rng.integers(5000, 35001, int(tail.sum()))
-            noff = np.zeros(args.seqs + 1, np.uint64)
-            np.cumsum(lens, out=noff[1:])
-            seg = np.repeat(np.arange(args.seqs), lens)
-            src = off[seg].astype(np.int64) + (np.arange(len(seg)) - noff[seg].astype(np.int64))
-            ncodes = syn._aa_lut()[rng.integers(0, 65536, size=len(seg), dtype=np.uint16)]
-            keep = ~tail[seg]
-            ncodes[keep] = codes[src[keep]]
-            codes, off = ncodes, noff
-            del seg, src, keep
+    if not dna and args.long_tail > 0:
+        # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
+        # residues of the DB's alphabet); the others keep theirs
+        codes, off = syn.with_long_tail(codes, off, args.long_tail, 77 + rank, args.alphabet)
     tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
     path = os.path.join(tmpdir, "db.fas")
     syn.write_fasta(path, codes, off, nucleotide=dna)
@@ -316,43 +474,65 @@ def main():
     S.set_id_offset(id0)
     S.prepare_db()
     os.remove(path)
+    os.rmdir(tmpdir)
     qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
     load_s = time.time() - t1
     setup_s = time.time() - t0
     cells_local = float(off[-1]) * args.qlen
+    total_cells = cells_local
+    if dist is not None:
+        # the shards are cut by residues: sum the ranks' cells
+        import torch
+        tc = torch.tensor([cells_local], dtype=torch.float64, device=dev)
+        dist.all_reduce(tc, op=dist.ReduceOp.SUM)
+        total_cells = float(tc.item())
 
     # N > 1: the shards' insertion logs meet on rank 0 in the library's own
     # RCCL gather (ssa_amd_gather_logs); the RCCL unique id travels over the
     # torch process group once
     native = world > 1 and backend == "nccl" and not args.torch_gather
     gather_note = None
+    rccl_ranks = None
     if native:
-        # every rank agrees on the path: a rank whose RCCL setup fails sends
-        # the whole job to the torch.distributed gather instead of leaving the
-        # others inside a collective
-        uid = None
-        if rank == 0:
-            try:
-                uid = S.dist_unique_id()
-            except RuntimeError as e:
-                gather_note = str(e)
-        obj = [uid]
-        dist.broadcast_object_list(obj, src=0)
-        ok = 0
-        if obj[0] is not None:
-            try:
-                S.dist_init(rank, world, obj[0])
-                ok = 1
-            except RuntimeError as e:
-                gather_note = str(e)
         import torch
-        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 0:
-            if ok:
-                S.dist_finalize()
+
+        def agree(ok):
+            # every rank takes the same path: MIN over the ranks' flags
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            return int(flag.item()) == 1
+        # 1. local readiness (RCCL resolvable, device selectable) agreed on
+        #    before anyone enters the collective ncclCommInitRank, so no rank
+        #    waits there for a peer that gave up
+        ready = S.dist_available()
+        if not ready:
+            gather_note = f"rank {rank}: RCCL not available to the library"
+        if agree(ready):
+            uid = None
+            if rank == 0:
+                try:
+                    uid = S.dist_unique_id()
+                except RuntimeError as e:
+                    gather_note = str(e)
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            ok = False
+            if obj[0] is not None:
+                try:
+                    S.dist_init(rank, world, obj[0])
+                    ok = True
+                except RuntimeError as e:
+                    gather_note = str(e)
+            if not agree(ok):
+                if ok:
+                    S.dist_finalize()
+                native = False
+                gather_note = gather_note or "RCCL setup failed on another rank"
+            else:
+                rccl_ranks = S.dist_ranks()
+        else:
             native = False
-            gather_note = gather_note or "RCCL setup failed on another rank"
+            gather_note = gather_note or "RCCL not available on another rank"
 
     def step():
         if world == 1:
@@ -374,14 +554,28 @@ def main():
         step()
     gather_checked = None
     if native:
-        # untimed: the RCCL gather's top-k must equal the torch.distributed
-        # gather of the same logs (every rank joins both collectives)
+        # untimed: the RCCL gather must equal the torch.distributed gather of
+        # the same logs -- this search's, and a synthetic rising log of 600
+        # rows per rank at k = 600 (longer than the 512-row slot: the
+        # exact-size ncclGather round).  Every rank joins every collective.
+        # On any disagreement the timed steps use the torch gather.
         from libssa_amd.dist import global_topk
         log = S.search(qq, algo, args.k, args.width, S.LOG)
-        a = S.gather_logs(log, args.k)
-        b = global_topk(log, args.k, dist, rank, world, dev)
-        if rank == 0:
-            gather_checked = [tuple(map(int, x[:2])) for x in a] == [tuple(map(int, x[:2])) for x in b]
+        long_log = [(1000 * (rank * 600 + i) + 7, 10 ** 6 * rank + i, 0, 0, 0) for i in range(600)]
+        same = True
+        for lg, kk in ((log, args.k), (long_log, 600)):
+            a = S.gather_logs(lg, kk)
+            b = global_topk(lg, kk, dist, rank, world, dev)
+            if rank == 0:
+                same = same and [tuple(map(int, x[:2])) for x in a] == [tuple(map(int, x[:2])) for x in b]
+        import torch
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=dev)
+        dist.broadcast(flag, src=0)
+        gather_checked = bool(int(flag.item()))
+        if not gather_checked:
+            S.dist_finalize()
+            native = False
+            gather_note = "RCCL gather disagreed with the torch.distributed gather: timed the torch gather"
     sync()
     kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms, upload_ms, sync_ms = [], [], [], [], [], [], [], []
     t_start = time.perf_counter()
@@ -415,7 +609,6 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    total_cells = cells_local * world
     ms_per_step = elapsed / args.steps * 1e3
     gcups = total_cells / (elapsed / args.steps) / 1e9
     kavg = float(np.mean(kernel_ms))
@@ -455,7 +648,7 @@ def main():
                                f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
                                f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
                    "db_seqs_per_gpu": args.seqs, "db_total_seqs": db_total, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
-                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "pair_strip_rows": st["strip_rows"], "strip_np": args.strip_np,
+                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "job_seqs": job_ids, "pair_strip_rows": st["strip_rows"], "strip_np": args.strip_np,
                    "bit_width": args.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -479,17 +672,21 @@ def main():
         "top_hit": list(res[0]) if res else None,
         "gather": ("ssa_amd_gather_logs (RCCL)" if native else "torch.distributed") if world > 1 else None,
         "gather_equals_torch_gather": gather_checked,
+        "rccl_ranks": rccl_ranks,
+        "launcher": os.environ.get("SSA_BENCH_LAUNCHER", "torchrun" if world > 1 else None),
     }
+    if ranks_per_gpu > 1:
+        out["rehearsal"] = f"{world} ranks on {max(1, world // ranks_per_gpu)} GPU(s), exchange over {backend}"
     if gather_note:
         out["gather_note"] = gather_note
     # the same DB and query as a reference-pinned fixture: the step's top-k
     # against the reference's own (tests/golden/fullsize.json)
     fxs = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))
-    job_ids = min(db_total, args.seqs * world)      # the whole job searches IDs [0, job_ids)
 
     def same_db(fx):
         return (fx.get("kind", "protein") == args.db and args.alphabet == fx.get("alphabet", "bg20")
                 and args.lengths == fx.get("lengths", "gamma") and fx["n"] == db_total and fx["i1"] == job_ids
+                and args.long_tail == fx.get("tail", 0) and fx.get("query_file") == cfg.get("query_file")
                 and fx["qlen"] == args.qlen and fx["algo"] == args.algo and fx["gap_open"] == args.gap_open
                 and fx["gap_extend"] == args.gap_extend and fx["matrix"] == args.matrix)
     # the fixture of this exact DB and search, if any (c2, c3, the c4 / c5
@@ -497,7 +694,7 @@ def main():
     # N = 8, c2x2/4/8 = C2's weak-scaling DBs): at N > 1 rank 0 holds the
     # gathered global top-k of the N shards
     fx = next((f for f in fxs.values() if same_db(f)), None)
-    if fx and args.long_tail == 0 and args.k in (1, 10, 64):
+    if fx and (args.long_tail == 0 or world == 1) and args.k in (1, 10, 64):
         out["topk_vs_reference"] = "match" if [list(x) for x in res] == fx[f"top{args.k}"] else "MISMATCH"
     if world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle as po

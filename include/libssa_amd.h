@@ -56,7 +56,8 @@ typedef struct {
     double upload_ms;        /* device time of the per-search uploads before the first kernel */
     double sync_wait_ms;     /* host time blocked in the final stream synchronisation */
     uint32_t strip_rows;     /* pair kernel: rows of its main strips (2 x "pair_np"); 0: other kernels */
-    uint32_t reserved;
+    uint32_t counters;       /* 1: overflow_8/16 were computed (bit width 64, output mode >= OUTPUT_INFO
+                                or option "counters" 1); 0: not computed, they read 0 */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -95,6 +96,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)
  *   "pair_ticket" 1|0    pair-kernel workgroups take the next groups in start order
  *                        (an atomic ticket; default) or in blockIdx order
+ *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
+ *                        m_run's INFO line): -1 (default) only at output mode
+ *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always
  * Unknown names print a warning. */
 void ssa_amd_set_option( const char * name, long value );
 
@@ -147,11 +151,34 @@ size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit
  * (counts[r] rows each), replayed in order through the reference heap. */
 int ssa_amd_dist_unique_id( void * id );
 size_t ssa_amd_dist_unique_id_bytes( void );
+/* Local readiness, no communication: 0 when RCCL resolves and this rank's
+ * device can be selected, i.e. everything ssa_amd_dist_init checks before it
+ * enters the collective ncclCommInitRank.  Agree on it across ranks (e.g. a
+ * MIN all-reduce) before calling ssa_amd_dist_init, so that no rank waits in
+ * the init for a peer that gave up. */
+int ssa_amd_dist_available( void );
 int ssa_amd_dist_init( int rank, int world, const void * id );
+/* Test support: the calling THREAD becomes rank `rank` of an in-process
+ * group of `world` threads (keyed by `group`), whose collectives exchange
+ * through host memory instead of RCCL -- the same slot layout, count rows and
+ * exact-size second round as over RCCL.  Released by ssa_amd_dist_finalize on
+ * that thread.  Returns 0 on success. */
+int ssa_amd_dist_init_fake( int rank, int world, int group );
+/* Ranks of the current communicator (ncclCommCount), 0 before init. */
+int ssa_amd_dist_ranks( void );
 void ssa_amd_dist_finalize( void );
 size_t ssa_amd_gather_logs( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit_t * out );
 size_t ssa_amd_merge_logs( const ssa_hit_t * rows, const size_t * counts, size_t nlogs, size_t stride,
                            size_t hitcount, ssa_hit_t * out );
+/* Residue-balanced contiguous shards: cuts records
+ * [0, n) with the given lengths into `world` ID ranges
+ * [bounds[r], bounds[r + 1]) (bounds has world + 1 entries, bounds[0] = 0,
+ * bounds[world] = n) whose residue sums are as equal as cuts at multiples of
+ * `align` allow (align = chunk_size keeps a multi-view search's chunk-
+ * interleaved insertion order the concatenation of the shards' orders;
+ * 0 or 1 = any record).  The multi-process analogue of ssa_amd_set_devices'
+ * split.  Returns 0, or 1 for world < 1. */
+int ssa_amd_shard_bounds( const uint64_t * lengths, size_t n, size_t world, size_t align, size_t * bounds );
 
 /* Persistent packed DB: ssa_amd_save_db writes the device
  * layout of the open DB (packing it first if needed); ssa_amd_load_db,

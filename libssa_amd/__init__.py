@@ -65,7 +65,7 @@ class ssa_amd_stats_t(Structure):
                 ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
                 ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64),
                 ("kernel", ctypes.c_char * 32), ("prep_ms", c_double), ("upload_ms", c_double),
-                ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("reserved", c_uint32)]
+                ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -82,7 +82,8 @@ EXPORTS = {
                       "ssa_amd_replay", "ssa_amd_query_views", "ssa_amd_translate", "ssa_amd_align_pair",
                       "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch",
                       "ssa_amd_dist_unique_id", "ssa_amd_dist_unique_id_bytes", "ssa_amd_dist_init",
-                      "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs", "ssa_amd_get_timeline"],
+                      "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs", "ssa_amd_get_timeline",
+                      "ssa_amd_dist_available", "ssa_amd_dist_init_fake", "ssa_amd_dist_ranks", "ssa_amd_shard_bounds"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -129,6 +130,9 @@ def load():
         "ssa_amd_merge_logs": ([POINTER(ssa_hit_t), POINTER(c_size_t), c_size_t, c_size_t, c_size_t,
                                 POINTER(ssa_hit_t)], c_size_t),
         "ssa_amd_get_timeline": ([c_void_p, c_size_t], c_size_t),
+        "ssa_amd_dist_available": ([], c_int), "ssa_amd_dist_init_fake": ([c_int, c_int, c_int], c_int),
+        "ssa_amd_dist_ranks": ([], c_int),
+        "ssa_amd_shard_bounds": ([c_void_p, c_size_t, c_size_t, c_size_t, POINTER(c_size_t)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -339,12 +343,40 @@ def dist_unique_id():
     return buf.raw
 
 
+def dist_available():
+    """ssa_amd_dist_available: True when this rank could enter ssa_amd_dist_init."""
+    return load().ssa_amd_dist_available() == 0
+
+
 def dist_init(rank, world, uid):
     if load().ssa_amd_dist_init(rank, world, uid) != 0:
         raise RuntimeError(f"ssa_amd_dist_init({rank}, {world}) failed")
 
 
+def dist_init_fake(rank, world, group=0):
+    """ssa_amd_dist_init_fake: the calling thread becomes rank `rank` of an
+    in-process group of `world` threads (test support)."""
+    if load().ssa_amd_dist_init_fake(rank, world, group) != 0:
+        raise RuntimeError(f"ssa_amd_dist_init_fake({rank}, {world}, {group}) failed")
+
+
+def dist_ranks():
+    """ssa_amd_dist_ranks: ranks of the communicator (ncclCommCount)."""
+    return load().ssa_amd_dist_ranks()
+
+
 def dist_finalize(): load().ssa_amd_dist_finalize()
+
+
+def shard_bounds(lengths, world, align=1):
+    """ssa_amd_shard_bounds: world + 1 record bounds of residue-balanced
+    contiguous shards (cuts at multiples of `align`)."""
+    import numpy as np
+    lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+    out = (c_size_t * (world + 1))()
+    if load().ssa_amd_shard_bounds(lens.ctypes.data, len(lens), world, align, out) != 0:
+        raise ValueError("ssa_amd_shard_bounds: world must be >= 1")
+    return [int(x) for x in out]
 
 
 def _hit_array(log):

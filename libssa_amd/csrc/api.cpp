@@ -153,6 +153,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     ssa_amd_stats_t& S = stats();
     S.overflow_8 = o8;
     S.overflow_16 = o16;
+    S.counters = (bw == BIT_WIDTH_64 || counters_on(cfg())) ? 1 : 0;
     S.replay_ms = t2 - t1;
     S.search_ms = now_ms() - t0;
     // m_run's bookkeeping messages (manager.c:147-170)
@@ -415,6 +416,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "pair_prio_groups")) cfg().pair_prio_groups = (int)value;
     else if (!strcmp(name, "timeline")) cfg().timeline = (int)value;
     else if (!strcmp(name, "pair_ticket")) cfg().pair_ticket = (int)value;
+    else if (!strcmp(name, "counters")) cfg().counters = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -40,12 +40,18 @@ struct Config {
     int long_groups = -1;                 // leading groups scored by long_kernel: -1 auto, 0 never, N forced
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
-    int long4_share_pct = 400;
+    int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
     int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)
-    int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)            // auto: 4 waves for groups longer than this % of a SIMD's share
+    int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
+                                          // >= INFO, when m_run prints them), 0 never, 1 always
+    int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
 };
 Config& cfg();
+// whether a search computes the overflow counters (Config::counters)
+inline bool counters_on(const Config& C) {
+    return C.counters > 0 || (C.counters < 0 && C.output_mode >= OUTPUT_INFO);
+}
 
 // SSA_AMD_TRACE=1: per-search host/device timing lines on stderr
 bool trace_on();

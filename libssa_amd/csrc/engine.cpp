@@ -448,28 +448,16 @@ std::vector<SlotPlan> device_plan() {
     static size_t chunk = 0, cnt = 0;
     static std::vector<SlotPlan> plan;
     if (gen == C.db_generation && devs == C.devices && chunk == C.chunk_size && cnt == count) return plan;
-    const size_t cs = C.chunk_size, nchunks = (count + cs - 1) / cs, n = C.devices.size();
-    std::vector<uint64_t> cum(nchunks + 1, 0);
-    for (size_t c = 0; c < nchunks; c++) {
-        uint64_t r = 0;
-        for (size_t i = c * cs; i < std::min(count, (c + 1) * cs); i++) {
-            p_seqinfo si = ssa_db_get_sequence(i);
-            if (si) r += si->seqlen;
-        }
-        cum[c + 1] = cum[c] + r;
+    const size_t n = C.devices.size();
+    std::vector<uint64_t> lens(count, 0);
+    for (size_t i = 0; i < count; i++) {
+        p_seqinfo si = ssa_db_get_sequence(i);
+        if (si) lens[i] = si->seqlen;
     }
+    std::vector<size_t> bounds(n + 1);
+    ssa_amd_shard_bounds(lens.data(), count, n, C.chunk_size, bounds.data());
     plan.clear();
-    size_t c0 = 0;
-    for (size_t s = 0; s < n; s++) {
-        size_t c1 = nchunks;
-        if (s + 1 < n) {
-            const uint64_t target = cum[nchunks] * (s + 1) / n;
-            c1 = (size_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-            c1 = std::max(c0, std::min(c1, nchunks));
-        }
-        plan.push_back({C.devices[s], std::min(count, c0 * cs), std::min(count, c1 * cs)});
-        c0 = c1;
-    }
+    for (size_t s = 0; s < n; s++) plan.push_back({C.devices[s], bounds[s], bounds[s + 1]});
     gen = C.db_generation;
     devs = C.devices;
     chunk = C.chunk_size;
@@ -773,8 +761,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.cand.clear();
     out.dev_o8 = out.dev_o16 = 0;
     // the reference's overflow counters (counters.hip): per (view, entry)
-    // flags, summed on the device after the last view
-    const bool want_counts = bw != BIT_WIDTH_64 && E > 0 && V > 0;
+    // flags, summed on the device after the last view -- only when someone
+    // observes them (m_run prints them at OUTPUT_INFO, manager.c:157-160;
+    // option "counters")
+    const bool want_counts = bw != BIT_WIDTH_64 && E > 0 && V > 0 && counters_on(cfg());
     bool counted = false;
     if (want_counts && D.flags_cap < V * E) {
         dfree(D.d_flags);
@@ -902,7 +892,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // 28-symbol DB: '-', U, O and X score alike against a standard-residue
         // query -> 25 classes, a 75.7 KiB table, two workgroups per CU instead
         // of none); the class-coded residues are cached per class map.
-                std::vector<uint8_t> cls_of, cls_rep;
+        std::vector<uint8_t> cls_of, cls_rep;
         {
             uint32_t qset = 0;
             for (size_t i = 0; i < m; i++) qset |= 1u << (qv.seq[i] & 31);
@@ -1233,7 +1223,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             la.gap_extend = R;
             // NW: the exact extremes of H the overflow counters decide from,
             // needed only when some long entry is too long for the bounds
-            // (2Q + (m + n4)R below the flag threshold; counters.hip)
             // (2Q + (m + n4)R below the flag threshold, or min(m, n4) maxM at
             // I_MAX: the decide kernel's bounds, counters.hip)
             bool need_hmm = false;

@@ -126,6 +126,30 @@ def _lut(codes: np.ndarray, probs: np.ndarray) -> np.ndarray:
     return codes[np.minimum(np.searchsorted(cdf, u), len(codes) - 1)].astype(np.uint8)
 
 
+def _protein_block(n: int, seed: int, b: int, query, plant_every: int, lo: int, hi: int, lengths: str):
+    """Block b's lengths, planted homologs and residue stream (the caller
+    draws the residues from the returned generator, after the lengths)."""
+    b0, b1 = b * BLOCK, min(n, (b + 1) * BLOCK)
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
+    if lengths == "gamma":
+        lens = np.clip(1 + np.rint(rng.gamma(2.0, 175.0, size=b1 - b0)), lo, hi).astype(np.int64)
+    else:
+        lens = rng.integers(lo, hi, size=b1 - b0).astype(np.int64)
+    plants = []
+    if query is not None and plant_every > 0:
+        prng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b, 1])))
+        first = b0 + ((plant_every // 2 - b0) % plant_every)
+        for pos in range(first, b1, plant_every):
+            hom = _mutate(prng, query)
+            lens[pos - b0] = len(hom)
+            plants.append((pos - b0, hom))
+    return b0, b1, lens, plants, rng
+
+
+def _blocks(i0: int, i1: int):
+    return range(i0 // BLOCK, (i1 + BLOCK - 1) // BLOCK if i1 > i0 else i0 // BLOCK)
+
+
 def protein_db_range(n: int, seed: int, i0: int = 0, i1: int | None = None, query: np.ndarray | None = None,
                      plant_every: int = 10000, lo: int = 16, hi: int = 4096, alphabet: str = "bg20",
                      lengths: str = "gamma"):
@@ -142,21 +166,8 @@ def protein_db_range(n: int, seed: int, i0: int = 0, i1: int | None = None, quer
     codes_a, probs_a = alphabet_table(alphabet)
     lut = _lut(codes_a, probs_a)
     parts, lens_all = [], []
-    for b in range(i0 // BLOCK, (i1 + BLOCK - 1) // BLOCK if i1 > i0 else i0 // BLOCK):
-        b0, b1 = b * BLOCK, min(n, (b + 1) * BLOCK)
-        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
-        if lengths == "gamma":
-            lens = np.clip(1 + np.rint(rng.gamma(2.0, 175.0, size=b1 - b0)), lo, hi).astype(np.int64)
-        else:
-            lens = rng.integers(lo, hi, size=b1 - b0).astype(np.int64)
-        plants = []
-        if query is not None and plant_every > 0:
-            prng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b, 1])))
-            first = b0 + ((plant_every // 2 - b0) % plant_every)
-            for pos in range(first, b1, plant_every):
-                hom = _mutate(prng, query)
-                lens[pos - b0] = len(hom)
-                plants.append((pos - b0, hom))
+    for b in _blocks(i0, i1):
+        b0, b1, lens, plants, rng = _protein_block(n, seed, b, query, plant_every, lo, hi, lengths)
         off = np.zeros(b1 - b0 + 1, dtype=np.int64)
         np.cumsum(lens, out=off[1:])
         codes = lut[rng.integers(0, 65536, size=int(off[-1]), dtype=np.uint16)]
@@ -172,6 +183,43 @@ def protein_db_range(n: int, seed: int, i0: int = 0, i1: int | None = None, quer
     return codes, off
 
 
+def protein_lengths_range(n: int, seed: int, i0: int = 0, i1: int | None = None, query: np.ndarray | None = None,
+                          plant_every: int = 10000, lo: int = 16, hi: int = 4096, lengths: str = "gamma"):
+    """The lengths of sequences [i0, i1) of protein_db_range's DB, without
+    drawing residues (cheap for a whole 10 M-sequence DB: bench.py's
+    residue-balanced shard cuts)."""
+    i1 = n if i1 is None else min(i1, n)
+    out = []
+    for b in _blocks(i0, i1):
+        b0, b1, lens, _, _ = _protein_block(n, seed, b, query, plant_every, lo, hi, lengths)
+        out.append(lens[max(i0, b0) - b0:min(i1, b1) - b0])
+    return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+
+def with_long_tail(codes: np.ndarray, off: np.ndarray, count: int, seed: int, alphabet: str = "bg20",
+                   lo: int = 5000, hi: int = 35000):
+    """A UniProt-like length tail: sequences 0, n//count, 2 n//count, ...
+    (count of them) are replaced by fresh i.i.d. residues of the alphabet with
+    lengths uniform in [lo, hi]; every other sequence keeps its residues.
+    Returns (codes, offsets)."""
+    n = len(off) - 1
+    if count <= 0 or n == 0:
+        return codes, off
+    rng = np.random.default_rng(seed)
+    lens = np.diff(off).astype(np.int64)
+    tail = np.zeros(n, bool)
+    tail[np.arange(count) * (n // count)] = True
+    lens[tail] = rng.integers(lo, hi + 1, int(tail.sum()))
+    noff = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=noff[1:])
+    seg = np.repeat(np.arange(n), lens)
+    src = off[seg].astype(np.int64) + (np.arange(len(seg)) - noff[seg].astype(np.int64))
+    ncodes = _lut(*alphabet_table(alphabet))[rng.integers(0, 65536, size=len(seg), dtype=np.uint16)]
+    keep = ~tail[seg]
+    ncodes[keep] = codes[src[keep]]
+    return ncodes, noff
+
+
 def dna_reads_range(n: int, seed: int, i0: int = 0, i1: int | None = None, length: int = 150,
                     query: np.ndarray | None = None, plant_every: int = 100000):
     """Reads [i0, i1) of the block-seeded n-read DNA DB (i.i.d. ACGT; every
@@ -179,7 +227,7 @@ def dna_reads_range(n: int, seed: int, i0: int = 0, i1: int | None = None, lengt
     substitutions)."""
     i1 = n if i1 is None else min(i1, n)
     parts = []
-    for b in range(i0 // BLOCK, (i1 + BLOCK - 1) // BLOCK if i1 > i0 else i0 // BLOCK):
+    for b in _blocks(i0, i1):
         b0, b1 = b * BLOCK, min(n, (b + 1) * BLOCK)
         rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
         codes = NT_ACGT[rng.integers(0, 4, size=(b1 - b0) * length, dtype=np.uint8)]

@@ -115,3 +115,197 @@ def test_native_rccl_gather_world1(tmp_path):
             assert S.gather_logs(log, k) == po.topk(sc, ids, k)
     finally:
         S.dist_finalize()
+
+
+def _fake_gather(logs, k, group):
+    """Runs ssa_amd_gather_logs from len(logs) host threads, each the rank of
+    an in-process group (ssa_amd_dist_init_fake); returns every rank's result
+    and the ranks each saw."""
+    import threading
+    import libssa_amd as S
+    W = len(logs)
+    res, ranks, errs = [None] * W, [None] * W, []
+
+    def run(r):
+        try:
+            S.dist_init_fake(r, W, group)
+            try:
+                ranks[r] = S.dist_ranks()
+                res[r] = S.gather_logs(logs[r], k)
+            finally:
+                S.dist_finalize()
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert not any(t.is_alive() for t in th), "fake collective did not drain"
+    assert not errs, errs
+    return res, ranks
+
+
+def _cuts(n, W, rng, empty):
+    c = np.sort(rng.integers(0, n + 1, W - 1))
+    if empty:
+        c[: max(1, (W - 1) // 2)] = c[0]       # some ranks get no records
+    return [0, *c.tolist(), n]
+
+
+@pytest.mark.parametrize("W", [2, 3, 8])
+@pytest.mark.parametrize("k", [1, 10, 300])
+@pytest.mark.parametrize("kind", ["ties", "rising", "empty"])
+def test_native_gather_fake_world(W, k, kind):
+    """ssa_amd_gather_logs at W > 1 without hardware: W threads exchange
+    through the library's in-process transport (the same slot layout, count
+    rows and exact-size second round as over RCCL).  Rank 0 gets the
+    single-process reference top-k (tie IDs included), the others nothing.
+    "rising" scores make every shard log longer than the 512-row slot at
+    k = 300, i.e. the ncclGather round; "empty" leaves ranks with no log."""
+    rng = np.random.default_rng(W * 1000 + k)
+    n = 6000
+    if kind == "rising":
+        sc = np.sort(rng.integers(0, 10 ** 6, n))
+    else:
+        sc = rng.integers(0, 40, n)
+    ids = np.arange(n, dtype=np.uint64)
+    cuts = _cuts(n, W, rng, kind == "empty")
+    logs = [[(int(s), int(i), 0, 0, 0) for s, i in po.topk_log(sc[a:b], ids[a:b], k)] for a, b in zip(cuts, cuts[1:])]
+    if kind == "rising" and k == 300:
+        assert max(len(x) for x in logs) > 512
+    res, ranks = _fake_gather(logs, k, group=W * 100 + k)
+    assert ranks == [W] * W
+    assert res[0] == po.topk(sc, ids, k)
+    assert all(r == [] for r in res[1:])
+
+
+def test_native_gather_fake_repeated_rounds():
+    """Several gathers on one fake group, alternating one- and two-round
+    exchanges (buffers grow and are reused): each equals the reference."""
+    import threading
+    import libssa_amd as S
+    W, rng = 4, np.random.default_rng(5)
+    cases = []
+    for j, k in enumerate((10, 600, 1, 600, 64)):
+        n = 4000
+        sc = np.sort(rng.integers(0, 10 ** 5, n)) if k == 600 else rng.integers(0, 30, n)
+        ids = np.arange(n, dtype=np.uint64)
+        cuts = _cuts(n, W, rng, False)
+        logs = [[(int(s), int(i), 0, 0, 0) for s, i in po.topk_log(sc[a:b], ids[a:b], k)]
+                for a, b in zip(cuts, cuts[1:])]
+        cases.append((logs, k, po.topk(sc, ids, k)))
+    out = [[] for _ in range(W)]
+
+    def run(r):
+        S.dist_init_fake(r, W, 999)
+        for logs, k, _ in cases:
+            out[r].append(S.gather_logs(logs[r], k))
+        S.dist_finalize()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert not any(t.is_alive() for t in th)
+    assert [x for x in out[0]] == [c[2] for c in cases]
+
+
+def test_native_gather_fake_refusals():
+    import libssa_amd as S
+    S.load()
+    assert S.dist_ranks() == 0
+    with pytest.raises(RuntimeError):
+        S.dist_init_fake(2, 2, 7)           # rank out of range
+    S.dist_init_fake(0, 2, 8)
+    with pytest.raises(RuntimeError):
+        S.dist_init_fake(1, 2, 8)           # this thread already holds a rank
+    S.dist_finalize()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("order", ["sorted", "reverse", "random"])
+def test_shard_bounds_balance_residues(world, order):
+    """ssa_amd_shard_bounds: contiguous ID ranges with residue sums within
+    1 % of each other on a length-sorted DB (where cutting by sequence count
+    would be off by ~10x), and at chunk-size multiples when asked."""
+    import libssa_amd as S
+    rng = np.random.default_rng(world)
+    lens = np.clip(1 + rng.gamma(2.0, 175.0, 200_000).round(), 16, 4096).astype(np.uint64)
+    if order == "sorted":
+        lens = np.sort(lens)
+    elif order == "reverse":
+        lens = np.sort(lens)[::-1].copy()
+    b = S.shard_bounds(lens, world)
+    assert b[0] == 0 and b[-1] == len(lens) and all(x <= y for x, y in zip(b, b[1:]))
+    res = [int(lens[x:y].sum()) for x, y in zip(b, b[1:])]
+    assert max(res) / min(res) <= 1.01, res
+    by_count = [int(lens[i * len(lens) // world:(i + 1) * len(lens) // world].sum()) for i in range(world)]
+    if order != "random":
+        assert max(by_count) / min(by_count) > 1.5
+    b = S.shard_bounds(lens, world, align=1000)
+    assert all(x % 1000 == 0 for x in b[:-1])
+    res = [int(lens[x:y].sum()) for x, y in zip(b, b[1:])]
+    assert max(res) / min(res) <= 1.1, res
+
+
+def test_shard_bounds_edges():
+    import libssa_amd as S
+    assert S.shard_bounds([], 3) == [0, 0, 0, 0]
+    assert S.shard_bounds([5], 1) == [0, 1]
+    b = S.shard_bounds([0, 0, 10, 0, 10, 0], 2)
+    assert b[0] == 0 and b[-1] == 6 and sum([0, 0, 10, 0, 10, 0][b[0]:b[1]]) == 10
+    with pytest.raises(ValueError):
+        S.shard_bounds([1, 2], 0)
+
+
+# ---------------------------------------------------------------- bench.py launcher
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launcher_spawns_ranks(world):
+    """`bench.py --gpus N` without a launcher starts N rank processes itself
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT), the ranks meet over
+    gloo, and the parent prints rank 0's single JSON line."""
+    import json
+    r = _bench(["--gpus", str(world), "--launch-selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["launch_selftest"] == "ok" and d["world"] == world
+    assert [x["rank"] for x in d["ranks"]] == list(range(world))
+    assert [x["local_rank"] for x in d["ranks"]] == list(range(world))
+    assert len({x["pid"] for x in d["ranks"]}) == world
+    assert all(x["launcher"] == "bench.py --gpus" for x in d["ranks"])
+
+
+def test_bench_launcher_propagates_failure():
+    """A rank that dies takes the job down: the parent stops the others
+    (which wait in the rendezvous for it) and exits with that rank's status."""
+    import time
+    t0 = time.time()
+    r = _bench(["--gpus", "3", "--launch-selftest", "--selftest-fail-rank", "1"], timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "rank 1 exited with status 3" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert time.time() - t0 < 90
+
+
+def test_bench_launcher_refuses_more_ranks_than_gpus():
+    """N > visible GPUs fails loudly instead of doubling ranks up (this
+    container has none)."""
+    r = _bench(["--gpus", "2", "--no-cpu-baseline"], env_extra={"SSA_DIST_BACKEND": "nccl"})
+    assert r.returncode == 2
+    assert "GPU(s) visible" in r.stderr

@@ -17,13 +17,23 @@ import pytest
 import libssa_amd as S
 from libssa_amd import synthetic as syn
 from oracle import pyoracle as po
-from tests.conftest import DATA, GOLDEN
+from tests.conftest import DATA, GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
 
 KATS = json.load(open(os.path.join(GOLDEN, "kat.json")))
 TABLES = np.load(os.path.join(GOLDEN, "tables.npz"))
 NAMES = [str(x) for x in TABLES["names"]]
+
+
+@pytest.fixture(autouse=True)
+def _counters_always():
+    """Most tests run at OUTPUT_ERROR and still assert the overflow counters:
+    ask for them explicitly (option "counters" 1; by default they are computed
+    only at OUTPUT_INFO, where m_run prints them)."""
+    S.set_option("counters", 1)
+    yield
+    S.set_option("counters", 1)
 
 
 def configure(nucleotide, spec, go, ge, chunk=1000, strands=S.FORWARD_STRAND):
@@ -53,6 +63,10 @@ API_KATS = [c for c in KATS if not (c["nucleotide"] and c["scoring"][0] != "cons
 @pytest.mark.parametrize("width", [S.BIT_WIDTH_16, S.BIT_WIDTH_8, S.BIT_WIDTH_64])
 def test_kat_public_api(case, width):
     configure(case["nucleotide"], case["scoring"], case["gap_open"], case["gap_extend"], case["chunk"])
+    # the default counter policy: computed because the output mode is INFO,
+    # as m_run prints them there (manager.c:157-160)
+    S.set_option("counters", -1)
+    S.set_output_mode(S.OUTPUT_INFO)
     S.init_db(os.path.join(DATA, case["db"]))
     q = make_query(case["query"])
     for algo, fn in (("sw", S.sw_align), ("nw", S.nw_align)):
@@ -65,6 +79,31 @@ def test_kat_public_api(case, width):
         exp = {S.BIT_WIDTH_8: tuple(case[algo + "_8_overflow"]), S.BIT_WIDTH_16: (0, case[algo + "_16_overflow"]),
                S.BIT_WIDTH_64: (0, 0)}[width]
         assert (st["overflow_8"], st["overflow_16"]) == exp, (algo, width)
+        assert st["counters"] == 1
+    S.free_sequence(q)
+
+
+@pytest.mark.parametrize("nw", [0, 1])
+def test_counters_skipped_when_unobserved(nw, tmp_path):
+    """At OUTPUT_ERROR with the default policy the counter kernels do not run
+    (stats counters = 0, overflow_8/16 read 0); the hits are unchanged, and
+    at OUTPUT_INFO the same search reports the reference's counts."""
+    case = next(c for c in API_KATS if c["name"] == "overflow_127")
+    configure(case["nucleotide"], case["scoring"], case["gap_open"], case["gap_extend"], case["chunk"])
+    S.set_option("counters", -1)
+    S.init_db(os.path.join(DATA, case["db"]))
+    q = make_query(case["query"])
+    fn = S.nw_align if nw else S.sw_align
+    algo = "nw" if nw else "sw"
+    quiet = [(h["score"], h["id"]) for h in fn(q, case["k"], S.BIT_WIDTH_8)]
+    st = S.stats()
+    assert (st["counters"], st["overflow_8"], st["overflow_16"]) == (0, 0, 0)
+    S.set_output_mode(S.OUTPUT_INFO)
+    loud = [(h["score"], h["id"]) for h in fn(q, case["k"], S.BIT_WIDTH_8)]
+    st = S.stats()
+    assert quiet == loud == [tuple(x) for x in case[algo + "_64"]]
+    assert st["counters"] == 1 and (st["overflow_8"], st["overflow_16"]) == tuple(case[algo + "_8_overflow"])
+    S.set_output_mode(S.OUTPUT_ERROR)
     S.free_sequence(q)
 
 
@@ -1089,17 +1128,26 @@ def _fullsize_inputs(c):
         q = syn.dna_query(c["qlen"], c["qseed"])
         codes, off = syn.dna_reads_range(c["n"], c["seed"], 0, c["i1"], 150, query=q)
         return q, codes, off
-    q = syn.protein_query(c["qlen"], c["qseed"])
+    q = _fullsize_query(c)
     codes, off = syn.protein_db_range(c["n"], c["seed"], 0, c["i1"], query=q, alphabet=c.get("alphabet", "bg20"),
                                       lengths=c.get("lengths", "gamma"), lo=c.get("lo", 16), hi=c.get("hi", 4096))
+    if c.get("tail"):
+        # a UniProt-like length tail (the "sprot" fixture: bench.py --config sprot)
+        codes, off = syn.with_long_tail(codes, off, c["tail"], c["tail_seed"], c.get("alphabet", "bg20"))
     return q, codes, off
+
+
+def _fullsize_query(c):
+    if c.get("query_file"):
+        lines = open(os.path.join(ROOT, c["query_file"])).read().split("\n")
+        seq = "".join(x.strip() for x in lines[1:] if not x.startswith(">")).upper()
+        return np.array([syn.AA_ORDER.index(ch) for ch in seq], dtype=np.uint8)
+    return syn.protein_query(c["qlen"], c["qseed"])
 
 
 # fixtures pinned by top-k and counters only (the GPU test does not pull their
 # multi-million-entry logs through Python)
 LARGE = ("c4full", "c5share8")
-# C2's weak-scaling DBs (bench.py at N = 2/4/8): pinned through the shard path
-SHARDED = ("c2x2",)
 
 
 @pytest.mark.parametrize("name", sorted(k for k in FULL if k not in LARGE and not k.startswith("c2x")))
@@ -1180,22 +1228,32 @@ def test_large_db_matches_reference(name, tmp_path):
     S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("name", [k for k in SHARDED if k in FULL])
-def test_sharded_db_logs_merge_to_reference_topk(name, tmp_path):
-    """bench.py's multi-GPU path at full size, on one GPU: C2's 2 M-sequence
-    weak-scaling DB searched as its two 1 M ID shards (each packed with its
-    global ID offset, ssa_amd_set_id_offset), their insertion logs merged by
-    the native shard merge (ssa_amd_merge_logs, what ssa_amd_gather_logs
-    runs on rank 0): top-1/10/64 equal the reference's own search of the
-    whole DB (tests/golden/fullsize.json)."""
+@pytest.mark.parametrize("name,world,balanced", [("c2x2", 2, False), ("c2x2", 3, True), ("c4full", 4, True)])
+def test_sharded_db_logs_merge_to_reference_topk(name, world, balanced, tmp_path):
+    """bench.py's multi-GPU path at full size, on one GPU: a fixture's DB
+    searched as `world` contiguous ID shards (each packed with its global ID
+    offset, ssa_amd_set_id_offset), their insertion logs merged by the native
+    shard merge (ssa_amd_merge_logs, what ssa_amd_gather_logs runs on rank 0):
+    top-1/10/64 equal the reference's own search of the whole DB
+    (tests/golden/fullsize.json).  C2's 2 M-sequence weak-scaling DB cut by
+    count (bench.py's weak shards at N = 2) and by residues into 3; C4's
+    whole 10 M DB cut by residues into 4 (ssa_amd_shard_bounds, bench.py's
+    strong shards at N = 4)."""
     c = FULL[name]
-    world = c["n"] // 1_000_000
-    q = syn.protein_query(c["qlen"], c["qseed"])
+    q = _fullsize_query(c)
     configure(False, ("builtin", c["matrix"]), c["gap_open"], c["gap_extend"])
+    if balanced:
+        lens = syn.protein_lengths_range(c["n"], c["seed"], 0, c["i1"], query=q)
+        cuts = S.shard_bounds(lens, world)
+        res = [int(lens[a:b].sum()) for a, b in zip(cuts, cuts[1:])]
+        assert max(res) / min(res) <= 1.01
+        del lens
+    else:
+        cuts = [r * c["i1"] // world for r in range(world + 1)]
     logs = []
     try:
         for r in range(world):
-            i0, i1 = r * 1_000_000, (r + 1) * 1_000_000
+            i0, i1 = cuts[r], cuts[r + 1]
             codes, off = syn.protein_db_range(c["n"], c["seed"], i0, i1, query=q, alphabet=c.get("alphabet", "bg20"),
                                               lo=16, hi=4096)
             path = os.path.join(str(tmp_path), f"db{r}.fas")

@@ -309,6 +309,12 @@ FULLSIZE = {
     "u28nw": dict(kind="protein", n=200_000, i1=200_000, seed=45, qlen=400, qseed=7, matrix="blosum62",
                   gap_open=-11, gap_extend=-1, algo="nw", width=16, alphabet="uniform28", lengths="uniform",
                   lo=16, hi=1000),
+    # the reference's own benchmark workload in Swiss-Prot's form (bench.py
+    # --config sprot): P18080 vs 548 208 sequences of the 25-symbol alphabet,
+    # BLOSUM50 -3/-1, 300 entries replaced by 5-35 k-residue ones
+    "sprot": dict(kind="protein", n=548_208, i1=548_208, seed=42, qlen=513, query_file="tests/golden/data/P18080.fasta",
+                  matrix="blosum50", gap_open=-3, gap_extend=-1, algo="sw", width=16, alphabet="sprot25",
+                  tail=300, tail_seed=77),
 }
 
 
@@ -318,9 +324,18 @@ def fullsize_db(c):
         q = syn.dna_query(c["qlen"], c["qseed"])
         codes, off = syn.dna_reads_range(c["n"], c["seed"], 0, c["i1"], 150, query=q)
         return q, codes, off
-    q = syn.protein_query(c["qlen"], c["qseed"])
+    if c.get("query_file"):
+        # the first record of the file, as bench.py reads it
+        lines = open(os.path.join(ROOT, c["query_file"])).read().split("\n")
+        seq = "".join(l.strip() for l in lines[1:] if not l.startswith(">")).upper()
+        q = np.array([syn.AA_ORDER.index(ch) for ch in seq], dtype=np.uint8)
+        assert len(q) == c["qlen"]
+    else:
+        q = syn.protein_query(c["qlen"], c["qseed"])
     codes, off = syn.protein_db_range(c["n"], c["seed"], 0, c["i1"], query=q, alphabet=c.get("alphabet", "bg20"),
                                       lengths=c.get("lengths", "gamma"), lo=c.get("lo", 16), hi=c.get("hi", 4096))
+    if c.get("tail"):
+        codes, off = syn.with_long_tail(codes, off, c["tail"], c["tail_seed"], c.get("alphabet", "bg20"))
     return q, codes, off
 
 
