@@ -416,6 +416,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "pair_prio_groups")) cfg().pair_prio_groups = (int)value;
     else if (!strcmp(name, "timeline")) cfg().timeline = (int)value;
     else if (!strcmp(name, "pair_ticket")) cfg().pair_ticket = (int)value;
+    else if (!strcmp(name, "pair_parts")) cfg().pair_parts = (int)value;
     else if (!strcmp(name, "counters")) cfg().counters = (int)value;
     else print_warning("unknown option %s", name);
 }

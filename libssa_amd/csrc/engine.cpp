@@ -51,6 +51,10 @@ void DeviceDB::release() {
     d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
     dfree(d_hmm);
     d_hmm = nullptr;
+    dfree(d_part);
+    dfree(d_smax);
+    d_part = d_smax = nullptr;
+    part_cap = smax_cap = 0;
     dfree(d_timeline);
     d_timeline = nullptr;
     timeline_cap = timeline_rows = 0;
@@ -375,7 +379,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     dalloc((void**)&D.d_frlist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
     // overflow counters, then the long-entry dispatch gate (TableArgs::gate)
     dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe + 16, "overflow counters");
-    check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe, hipHostMallocDefault), "pinned");
+    check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe + 16, hipHostMallocDefault), "pinned");
     D.upblk_cap = kUpHeader + 16384 + 4096;
     dalloc((void**)&D.d_upblk, D.upblk_cap, "per-search uploads");
     D.d_matrix = (int64_t*)D.d_upblk;
@@ -870,6 +874,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     uint64_t kernel_bytes = 0;
     const char* kname = "";
     uint32_t srows = 0;
+    bool parts_used = false;                 // some view ran strip parts (their wait-timeout word is read back)
 
     for (size_t v = 0; v < V; v++) {
         const QueryView& qv = views[v];
@@ -1329,6 +1334,39 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 const uint32_t pg = C.pair_prio_groups < 0 ? D.nsimd : (uint32_t)C.pair_prio_groups;
                 b.g_prio = (uint32_t)std::min<uint64_t>((uint64_t)long_groups + pg, D.ngroups);
             }
+            // strip parts: the launch's last work units become a fraction of a
+            // group (kernels.h StripArgs::nparts)
+            {
+                const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
+                uint32_t parts = C.pair_parts > 0 ? (uint32_t)C.pair_parts : 1u;
+                parts = std::min(parts, T);
+                if (parts > 1 && D.ngroups > long_groups) {
+                    const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
+                    const uint32_t ps = (T + parts - 1) / parts;
+                    parts = (T + ps - 1) / ps;
+                    if (D.part_cap < quads || D.smax_cap < (size_t)D.ngroups * 64) {
+                        if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                        if (D.part_cap < quads) {
+                            dfree(D.d_part);
+                            check(hipMalloc((void**)&D.d_part, (size_t)quads * 4), "strip parts");
+                            D.part_cap = quads;
+                        }
+                        if (D.smax_cap < (size_t)D.ngroups * 64) {
+                            dfree(D.d_smax);
+                            check(hipMalloc((void**)&D.d_smax, (size_t)D.ngroups * 64 * 4), "strip-part maxima");
+                            D.smax_cap = (size_t)D.ngroups * 64;
+                        }
+                    }
+                    check(hipMemsetAsync(D.d_part, 0, (size_t)quads * 4, st), "memset");
+                    b.nparts = parts;
+                    b.part_strips = ps;
+                    b.nquads = quads;
+                    b.part_done = D.d_part;
+                    b.part_smax = D.d_smax;
+                    b.part_err = gate + 2;
+                    parts_used = true;
+                }
+            }
             const int lnp = main_strips ? pnp : tail_np;
             check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
@@ -1477,10 +1515,13 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * (pre + 1), hipMemcpyDeviceToHost, st), "D2H overflow");
             check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * pre, hipMemcpyDeviceToHost, st), "D2H wide");
         }
+        uint32_t* const h_perr = (uint32_t*)(D.h_cnt + 2 * kMaxBatchPipe) + 2;
+        if (parts_used) check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
         check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
         check(hipStreamSynchronize(st), "search");
         sync_wait += now_ms() - t_sync0;
+        if (parts_used && *h_perr) fatal("pair kernel: a strip part waited more than 0.5 s for its predecessor");
         const double t_post0 = now_ms();
 
         {

@@ -93,7 +93,12 @@ struct DeviceDB {
     uint32_t* d_entry_lane = nullptr;     // [entries] (length, lane) in entry order
     size_t hmm_cap = 0;                   // lanes
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
-    unsigned long long* h_cnt = nullptr;  // pinned mirror
+    unsigned long long* h_cnt = nullptr;  // pinned mirror (+ 16 B: the gate block's error word)
+    // pair_kernel strip parts (StripArgs::nparts): per quad parts done, per lane running maxima
+    uint32_t* d_part = nullptr;
+    size_t part_cap = 0;
+    uint32_t* d_smax = nullptr;
+    size_t smax_cap = 0;
     // long entries (long_kernel, launched on stream_long beside the pair
     // kernel): the groups' column counts (longest first), their sum, the
     // device's SIMD count, the multi-pass scratch

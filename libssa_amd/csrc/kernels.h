@@ -54,6 +54,21 @@ struct StripArgs {
     // XCD still gets an equal share; tickets hand the next-longest groups to
     // whichever workgroup starts next on any XCD.  Null: blockIdx order.
     uint32_t* ticket;
+    // pair_kernel: each group's strips in `nparts` consecutive parts of
+    // `part_strips` strips (the tail strip counts as one), run as separate
+    // work units: unit u = part (u / nquads) of quad (u % nquads), so the
+    // units of all groups' first parts come first (longest groups first),
+    // then all second parts, ...  A part waits until its group's previous
+    // part is done (part_done[quad], release/acquire at agent scope: the
+    // strip boundary rows cross workgroups, maybe XCDs); the SW running
+    // maximum travels in part_smax (one dword per lane).  The launch's last
+    // units are then the shortest groups' last parts -- a fraction of a
+    // whole group's work -- so the SIMDs drain together.
+    // nparts 1: whole groups, no carry.
+    uint32_t nparts, part_strips, nquads;
+    uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)
+    uint32_t* part_smax;       // [ngroups * 64]
+    uint32_t* part_err;        // set when a wait timed out (the host then refuses the result)
 };
 
 // Long DB entries (long_kernel): the query rows split over the lanes of W

@@ -519,6 +519,30 @@ pair_kernel(const StripArgs a) {
         __syncthreads();
         wg = __builtin_amdgcn_readfirstlane(lds[0]);
     }
+    // strip parts (StripArgs::nparts): unit wg = part `part` of quad wg
+    uint32_t part = 0;
+    if (a.nparts > 1) {
+        part = wg / a.nquads;
+        wg -= part * a.nquads;
+        if (part > 0) {
+            // the group's previous part must be done: its strip boundary rows
+            // (row buffer) and running maxima come from that workgroup.  Its
+            // unit had a lower ticket, so it is resident or finished: the wait
+            // ends (bounded anyway -- a timeout is reported, never a hang)
+            if (threadIdx.x == 0) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(a.part_done + wg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < part) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {       // 0.5 s
+                        __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            __syncthreads();
+            __threadfence();
+        }
+    }
     const uint32_t g = a.g_first + wg * W + wave;
     const bool active = g < a.ngroups;
     if (g < a.g_prio) __builtin_amdgcn_s_setprio(2);
@@ -544,7 +568,7 @@ pair_kernel(const StripArgs a) {
     // an exact H_max + (-|R|) unless it is 0 (then the lane is re-scored)
     const uint32_t Rabs = (uint32_t)(-R);
     const uint32_t cRabs = Rabs * 0x10001u;
-    uint32_t S = 0;
+    uint32_t S = (!NW && part > 0 && active) ? a.part_smax[gl] : 0u;
     // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
     uint32_t cap = 0;
     int cap_half = 0;
@@ -806,11 +830,25 @@ pair_kernel(const StripArgs a) {
 
     using MainNP = std::integral_constant<int, NP>;
     using TailNP = std::integral_constant<int, NPT ? NPT : 8>;
-    for (int s = 0; s < (int)a.nstrips; s++)
-        strip(MainNP{}, std::false_type{}, s * 2 * NP, a.qpt + (size_t)s * prow * prow * NP);
-    if (NPT > 0)
+    // this unit's strips [s0, s1) of the nstrips main strips + the tail strip
+    const uint32_t T = a.nstrips + (NPT > 0 ? 1u : 0u);
+    const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
+    const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
+    for (uint32_t s = s0; s < min(s1, a.nstrips); s++)
+        strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, a.qpt + (size_t)s * prow * prow * NP);
+    if (NPT > 0 && s1 == T)
         strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, a.qpt_tail);
 
+    if (a.nparts > 1 && part + 1 < a.nparts) {
+        // hand the group on: running maxima, then (after every wave's row
+        // buffer stores and maxima are visible at agent scope) the part count
+        if (!NW && active) a.part_smax[gl] = S;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.part_done + wg, part + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (!active) return;
     if (a.timeline && lane == 0)
         a.timeline[g - a.g_first] = make_uint4(g, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
@@ -1599,7 +1637,9 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     const hipError_t e = lds_attr_once((const void*)pair_kernel<NP, NW, NPT>, attr, (int)kPairLdsMax);
     if (e != hipSuccess) return e;
     constexpr int W = pair_waves(NP, NW);
-    const uint32_t blocks = (a.ngroups - a.g_first + W - 1) / W;
+    const uint32_t quads = (a.ngroups - a.g_first + W - 1) / W;
+    if (a.nparts > 1 && a.nquads != quads) return hipErrorInvalidValue;
+    const uint32_t blocks = quads * std::max(a.nparts, 1u);
     hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }

@@ -356,6 +356,46 @@ def test_wave_timeline_and_priority_keep_scores():
         S.free_sequence(qq)
 
 
+@pytest.mark.parametrize("algo,qlen", [(S.SW, 300), (S.SW, 49), (S.NW, 1000), (S.NW, 90)])
+def test_strip_parts_keep_scores(algo, qlen):
+    """pair_kernel with each group's strips split into dependent work units
+    (option "pair_parts": all groups' first parts, then the second, ...; the
+    strip boundary rows and SW running maxima cross workgroups): every score
+    equals the oracle's for 2, 3 and one part per strip (more parts than
+    strips clamp), with and without long_kernel groups and start-order
+    tickets."""
+    rng = np.random.default_rng(qlen)
+    q = syn.protein_query(qlen, 77 + qlen)
+    lens = np.array([3000, 2800, 2600, 0, 1] + list(rng.integers(1, 500, 3000)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    codes[int(off[10]):int(off[10]) + min(qlen, int(lens[10]))] = q[:min(qlen, int(lens[10]))]
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            for parts, lg, ticket in ((2, -1, 1), (3, 0, 1), (50, 1, 1), (3, 2, 0), (1, -1, 1)):
+                S.set_option("pair_parts", parts)
+                S.set_option("long_groups", lg)
+                S.set_option("pair_ticket", ticket)
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all()
+                assert (sc == exp).all(), (parts, lg, ticket, np.nonzero(sc != exp)[0][:10])
+                assert S.stats()["kernel"].startswith("pair_f16")
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, keep.astype(np.uint64), 10)
+        finally:
+            S.set_option("pair_parts", 1)
+            S.set_option("long_groups", -1)
+            S.set_option("pair_ticket", 1)
+        S.free_sequence(qq)
+
+
 @pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 @pytest.mark.parametrize("waves", [4, 1])
