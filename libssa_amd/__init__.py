@@ -19,7 +19,8 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int8, c_long
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libssa_amd.so")
+# SSA_AMD_LIB: an alternative build of the library (A/B measurements only)
+LIB_PATH = os.environ.get("SSA_AMD_LIB") or os.path.join(LIB_DIR, "libssa_amd.so")
 DB_LIB_PATH = os.path.join(LIB_DIR, "libssa_fasta_db.so")
 
 # ---- constants (libssa.h) ---------------------------------------------------

@@ -2,6 +2,7 @@
 // reference's src/libssa.h:122-263, implemented in src/libssa.c) plus the
 // MI355X extensions of include/libssa_amd.h.
 #include <algorithm>
+#include <numeric>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -417,6 +418,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "timeline")) cfg().timeline = (int)value;
     else if (!strcmp(name, "pair_ticket")) cfg().pair_ticket = (int)value;
     else if (!strcmp(name, "pair_parts")) cfg().pair_parts = (int)value;
+    else if (!strcmp(name, "batch_fuse")) cfg().batch_fuse = (int)value;
     else if (!strcmp(name, "counters")) cfg().counters = (int)value;
     else print_warning("unknown option %s", name);
 }
@@ -458,22 +460,31 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
     }
     if (piped) {
         DeviceDB& D = device_db(0);
+        // sub-batches of queries of similar length (stable order by length):
+        // a sub-batch whose pair-kernel plans agree runs as one fused launch
+        std::vector<size_t> ord(nq);
+        std::iota(ord.begin(), ord.end(), (size_t)0);
+        std::stable_sort(ord.begin(), ord.end(),
+                         [&](size_t x, size_t y) { return qviews[x][0].len < qviews[y][0].len; });
+        uint32_t launches = 0;
         for (size_t b0 = 0; b0 < nq; b0 += kMaxBatchPipe) {
             const size_t b1 = std::min(nq, b0 + kMaxBatchPipe);
             std::vector<QueryView> vs;
-            for (size_t i = b0; i < b1; i++) vs.push_back(qviews[i][0]);
+            for (size_t i = b0; i < b1; i++) vs.push_back(qviews[ord[i]][0]);
             if (vs.size() == 1) {
                 // a lone last query: the ordinary path
+                const size_t qi = ord[b0];
                 SearchResult R;
-                run_search(queries[b0], al, hitcount, bit_width, false, R);
+                run_search(queries[qi], al, hitcount, bit_width, false, R);
                 kms += stats().kernel_ms;
                 cells += stats().cells;
+                launches++;
                 const size_t n = std::min(hitcount, R.hits.size());
                 for (size_t j = 0; j < n; j++) {
                     const Hit& h = R.hits[j];
-                    out[b0 * hitcount + j] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
+                    out[qi * hitcount + j] = ssa_hit_t{h.score, h.id, h.qid, h.strand, h.frame, {0, 0, 0, 0, 0}};
                 }
-                if (counts) counts[b0] = n;
+                if (counts) counts[qi] = n;
                 total += n;
                 continue;
             }
@@ -481,8 +492,10 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
             std::vector<SearchScores> sc;
             device_search(D, vs, al, hitcount, bit_width, agg, &sc);
             kms += agg.kernel_ms;
-            for (size_t i = b0; i < b1; i++) {
-                const SearchScores& x = sc[i - b0];
+            launches += agg.fused_views ? 1u : (uint32_t)vs.size();
+            for (size_t bi = b0; bi < b1; bi++) {
+                const size_t i = ord[bi];
+                const SearchScores& x = sc[bi - b0];
                 cells += x.cells;
                 TopK heap(hitcount);
                 replay(x, D.meta, qviews[i], heap, nullptr);
@@ -499,6 +512,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         ssa_amd_stats_t& S = stats();
         S.kernel_ms = kms;
         S.cells = cells;
+        S.kernel_launches = launches;
         S.search_ms = now_ms() - t0;
         return total;
     }

@@ -43,6 +43,7 @@ struct Config {
     int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
     int pair_parts = 1;                   // pair_kernel: each group's strips in N dependent parts (StripArgs::nparts),
                                           // 1 whole groups, 0 auto
+    int batch_fuse = 1;                   // ssa_amd_search_batch: queries of one pair-kernel plan in one launch
     int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode

@@ -5,6 +5,7 @@
 // re-fetches and re-maps every sequence on every search) and its per-thread
 // SIMD drivers (search_16.c:92-134, search_8.c:94-146).
 #include <algorithm>
+#include <functional>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -55,6 +56,9 @@ void DeviceDB::release() {
     dfree(d_smax);
     d_part = d_smax = nullptr;
     part_cap = smax_cap = 0;
+    dfree(d_rowbuf_q);
+    d_rowbuf_q = nullptr;
+    rowbuf_q_cap = 0;
     dfree(d_timeline);
     d_timeline = nullptr;
     timeline_cap = timeline_rows = 0;
@@ -713,7 +717,8 @@ static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
     return 24;
 }
 
-static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM) {
+static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
+                          uint32_t scale = 1) {
     const Config& C = cfg();
     const uint32_t need = (uint32_t)((beyond + 63) / 64);
     if (C.long_groups == 0 || D.ngroups == 0 || D.alpha > 32) return need ? UINT32_MAX : 0;
@@ -730,11 +735,185 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
         // (a lower threshold costs more than it gains: long_kernel's cost per
         // cell is several times pair_kernel's -- the 548 k-entry DB: 40 %
         // 9.7, 50 % 10.9, 65 % 10.9 TCUPS)
-        const double thr = (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0;
+        const double thr = (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0 * scale;
         while (g < D.ngroups && g < kLongMaxGroups && D.group_ncols[g] > thr) g++;
     }
     g = std::max(g, need);
     return need > kLongMaxGroups ? UINT32_MAX : g;
+}
+
+// The kernels and bounds that score one query view (device_search):
+// residue classes, profile bounds, pair-kernel admissibility and strip plan,
+// long-entry groups.  Host only, no device work.  `force` (a fused batch,
+// one pair_kernel launch for several queries): the profile bounds and the
+// row count the length limits are computed for, shared by all its queries,
+// and the factor by which the launch outlasts one query's (long groups).
+struct ViewPlan {
+    std::vector<uint8_t> cls_of, cls_rep;
+    bool use_cls = false;
+    uint32_t A = 0, prow = 0;
+    int64_t minM = 0, maxM = 0;
+    uint32_t nmax16 = 0, nw_base = 0, long_groups = 0;
+    int pnp = 0;
+    size_t pair_lds = 0;
+    bool use_pair = false, use_f16 = false;
+    uint32_t nstrips = 0;
+    int rel = 0;
+    int16_t padv = 0;
+    uint32_t main_strips = 0;
+    int tail_np = 0;
+    size_t tail_off = 0, qpt_words = 0;   // pair tables: tail offset, total dwords
+};
+struct PlanForce {
+    int64_t minM, maxM;
+    size_t m;
+    uint32_t long_scale;
+};
+
+static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, const PlanForce* force, ViewPlan& vp) {
+    const Config& C = cfg();
+    const int Q = C.gap_open, R = C.gap_extend;
+    const int64_t* M = matrix().m;
+    const size_t m = qv.len;
+    const size_t ml = force ? force->m : m;        // row count of the length limits
+    std::vector<uint8_t>& cls_of = vp.cls_of;
+    std::vector<uint8_t>& cls_rep = vp.cls_rep;
+    // residue classes of this view: DB codes whose matrix rows agree on
+    // every residue of the query score identically, so the kernels may
+    // see one code per class.  Used when it lets more pair-kernel
+    // workgroups share a CU's LDS (the reference generator's uniform
+    // 28-symbol DB: '-', U, O and X score alike against a standard-residue
+    // query -> 25 classes, a 75.7 KiB table, two workgroups per CU instead
+    // of none); the class-coded residues are cached per class map.
+    {
+        uint32_t qset = 0;
+        for (size_t i = 0; i < m; i++) qset |= 1u << (qv.seq[i] & 31);
+        cls_of.resize(D.alpha);
+        for (uint32_t c = 0; c < D.alpha; c++) {
+            const int64_t* rc = M + ((size_t)D.code_of[c] << 5);
+            size_t k = 0;
+            for (; k < cls_rep.size(); k++) {
+                const int64_t* rk = M + ((size_t)cls_rep[k] << 5);
+                bool same = true;
+                for (int y = 0; y < 32 && same; y++) same = !((qset >> y) & 1) || rc[y] == rk[y];
+                if (same) break;
+            }
+            if (k == cls_rep.size()) cls_rep.push_back(D.code_of[c]);
+            cls_of[c] = (uint8_t)k;
+        }
+    }
+    // (workgroups per CU, strip height) of the pair kernel for a compact
+    // alphabet of a codes
+    auto pair_wgs = [&](size_t a) {
+        const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1, m);
+        const size_t b = (a + 1) * (a + 1) * (pn + 4) * 4;
+        const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
+        return std::make_pair(w, pn);
+    };
+    const bool use_cls = vp.use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
+                         pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
+    const std::vector<uint8_t>& code_of = use_cls ? cls_rep : D.code_of;
+    // profile bounds over the residue codes the DB holds
+    const uint32_t A = (uint32_t)code_of.size();
+    int64_t minM = INT64_MAX, maxM = INT64_MIN;
+    for (size_t i = 0; i < m; i++)
+        for (uint32_t c = 0; c < A; c++) {
+            const int64_t x = M[(code_of[c] << 5) + qv.seq[i]];
+            minM = std::min(minM, x);
+            maxM = std::max(maxM, x);
+        }
+    if (A == 0) minM = maxM = 0;
+    if (force) {
+        minM = force->minM;
+        maxM = force->maxM;
+    }
+    const bool fits16 = minM >= -32768 && maxM <= 32767;
+    uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(ml, Q, R, minM, maxM) : 0xffffffffu) : 0;
+    // SW with a positive gap increment (R > 0 or Q + R > 0): E would keep
+    // growing through the strip kernels' padding columns past an entry's
+    // end and leak into its maximum -- every lane goes to the exact int64
+    // kernel (the reference's full_sw recurrence)
+    if (!nw && (R > 0 || Q + R > 0)) nmax16 = 0;
+    if (C.force_wide) nmax16 = 0;
+    // SW on f16 bit patterns needs non-positive gaps and scores within
+    // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
+    const uint32_t prow = A + 1;
+    // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
+    const int pnp = pair_strip_np(C.pair_np, nw, prow, m);
+    const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
+    // pair kernel (diagonal-relative f16 patterns): only when no more than
+    // a handful of entries exceed its length bound (those are re-scored
+    // by the int64 kernel); otherwise the strip kernels
+    uint32_t nw_base = 0;
+    bool use_pair = false;
+    uint32_t long_groups = 0;            // leading groups scored by long_kernel
+    if (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
+        uint32_t lim = nw ? nw_f16_limit(ml, Q, R, minM, maxM, &nw_base) : sw_rel_limit(ml, Q, R, minM, maxM);
+        lim = std::min(lim, nmax16);
+        if (lim > 0) {
+            const size_t beyond = (size_t)(D.len_sorted.end() -
+                                           std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
+            const uint32_t lg = long_plan(D, ml, beyond, Q, R, minM, maxM, force ? force->long_scale : 1u);
+            // (an entry beyond the bound would also corrupt its group's
+            // other lanes, whose padding columns run to its length: the
+            // group must go to long_kernel, or the strip kernels run)
+            if (lg != UINT32_MAX) {
+                use_pair = true;
+                nmax16 = lim;
+                long_groups = lg == UINT32_MAX ? 0 : lg;
+            }
+        }
+    }
+    // SW on f16 patterns without the pair table (strip_f16m_kernel) needs
+    // non-positive gaps and scores within +-1024
+    const bool use_f16 = use_pair || (!nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024);
+    // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
+    // pair table of a strip of height 2P from row i0,
+    //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
+    const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
+    // NW on the pair kernel is diagonal-relative: every profile value (and
+    // the padding value 0) carries -2R
+    const int rel = use_pair ? -2 * R : 0;
+    const int16_t padv = nw ? (int16_t)rel : (use_f16 ? (int16_t)(-1024 + rel) : -32768);
+    // pair kernel plan (one launch): main strips of 2*pnp rows, then a
+    // tail strip of the smallest height (multiple of 8 rows) that holds the
+    // remainder; NW always ends in a tail strip, which captures its score
+    size_t qpt_words = 0;                // device table size (dwords)
+    uint32_t main_strips = 0;
+    int tail_np = 0;
+    size_t tail_off = 0;
+    if (use_pair) {
+        const uint32_t Hm = 2 * pnp;
+        uint32_t full = (uint32_t)(m / Hm);
+        const uint32_t rem = (uint32_t)(m % Hm);
+        if (rem > 0) {
+            tail_np = (int)(rem + 7) / 8 * 4;     // 8-row granularity
+        } else if (nw) {
+            full--;
+            tail_np = pnp;
+        }
+        main_strips = full;
+        tail_off = (size_t)full * prow * prow * pnp;
+        qpt_words = tail_off + (size_t)prow * prow * tail_np;
+    }
+    vp.A = A;
+    vp.prow = prow;
+    vp.minM = minM;
+    vp.maxM = maxM;
+    vp.nmax16 = nmax16;
+    vp.nw_base = nw_base;
+    vp.long_groups = long_groups;
+    vp.pnp = pnp;
+    vp.pair_lds = pair_lds;
+    vp.use_pair = use_pair;
+    vp.use_f16 = use_f16;
+    vp.nstrips = nstrips;
+    vp.rel = rel;
+    vp.padv = padv;
+    vp.main_strips = main_strips;
+    vp.tail_np = tail_np;
+    vp.tail_off = tail_off;
+    vp.qpt_words = qpt_words;
 }
 
 bool batch_pipelinable(size_t nqueries, size_t k) {
@@ -869,6 +1048,83 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             D.order_key = key;
         }
     }
+    // a batch of single-view queries whose pair-kernel plans agree (strip
+    // heights and counts; no residue classes) runs as ONE pair_kernel launch
+    // over all of them (StripArgs::nq): the launch's ramp and drain are paid
+    // once per batch instead of once per query, and a short query's strips
+    // share the chip with the others'.  The profile bounds (and so the f16
+    // length limit, NW base and long-entry routing) are the batch's union;
+    // each query keeps its own tables, scores, overflow list, filter pass.
+    bool fused = false;
+    std::vector<ViewPlan> fplans;
+    size_t fstride = 0;                  // per-query upload block / staging stride
+    StripArgs fb{};                      // view 0's pair-kernel arguments
+    std::vector<std::function<void()>> deferred;
+    if (ind && V > 1 && V <= (size_t)kMaxFuse && C.batch_fuse && !C.timeline && E > 0) {
+        fplans.resize(V);
+        fused = true;
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        size_t mmax = 0;
+        for (size_t v = 0; v < V && fused; v++) {
+            plan_view(D, views[v], nw, np, nullptr, fplans[v]);
+            const ViewPlan &p = fplans[v], &p0 = fplans[0];
+            fused = p.use_pair && !p.use_cls && p.pnp == p0.pnp && p.main_strips == p0.main_strips &&
+                    p.tail_np == p0.tail_np;
+            lo = std::min(lo, p.minM);
+            hi = std::max(hi, p.maxM);
+            mmax = std::max(mmax, views[v].len);
+        }
+        if (fused) {
+            const PlanForce f{lo, hi, mmax, (uint32_t)V};
+            for (size_t v = 0; v < V && fused; v++) {
+                plan_view(D, views[v], nw, np, &f, fplans[v]);
+                const ViewPlan &p = fplans[v], &p0 = fplans[0];
+                fused = p.use_pair && !p.use_cls && p.pnp == p0.pnp && p.main_strips == p0.main_strips &&
+                        p.tail_np == p0.tail_np && p.long_groups == p0.long_groups && p.nmax16 == p0.nmax16 &&
+                        p.nw_base == p0.nw_base && p.qpt_words == p0.qpt_words;
+            }
+            // NW counters read the long entries' exact extremes from one
+            // buffer per search: not shared between deferred views
+            if (fused && want_counts && nw && fplans[0].long_groups > 0) fused = false;
+        }
+        if (fused) {
+            const size_t ncols_max = ((size_t)(D.len_sorted.empty() ? 0 : D.len_sorted.back()) + 1 + 3) & ~(size_t)3;
+            const size_t top_bytes = (std::max<size_t>(ncols_max, 4) * 4 + 15) & ~(size_t)15;
+            fstride = (kUpHeader + top_bytes + mmax + 16 + 255) & ~(size_t)255;
+            const size_t qw = fplans[0].qpt_words;
+            const bool rows_cross = fplans[0].main_strips + (fplans[0].tail_np > 0 ? 1u : 0u) > 1;
+            const size_t rb = rows_cross ? V * (size_t)D.nblocks * 4096 : 0;
+            if (rb > D.rowbuf_q_cap) {
+                // one row buffer per query: only within a third of the free memory
+                size_t fr = 0, tot = 0;
+                check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
+                if (rb > fr / 3) fused = false;
+            }
+            if (fused) {
+                check(hipStreamSynchronize(D.stream), "sync");
+                if (D.upblk_cap < V * fstride) {
+                    dfree(D.d_upblk);
+                    D.upblk_cap = V * fstride;
+                    check(hipMalloc((void**)&D.d_upblk, D.upblk_cap), "per-search uploads");
+                }
+                if (D.h_up_cap < V * fstride) {
+                    if (D.h_up) (void)hipHostFree(D.h_up);
+                    check(hipHostMalloc((void**)&D.h_up, V * fstride, hipHostMallocDefault), "pinned uploads");
+                    D.h_up_cap = V * fstride;
+                }
+                if (D.qpt_cap < V * qw) {
+                    dfree(D.d_qpt);
+                    check(hipMalloc((void**)&D.d_qpt, V * qw * 4), "qpt");
+                    D.qpt_cap = V * qw;
+                }
+                if (rb > D.rowbuf_q_cap) {
+                    dfree(D.d_rowbuf_q);
+                    check(hipMalloc((void**)&D.d_rowbuf_q, rb), "per-query row buffers");
+                    D.rowbuf_q_cap = rb;
+                }
+            }
+        }
+    }
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
     uint64_t kernel_bytes = 0;
@@ -890,41 +1146,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (want_counts) check(hipMemsetAsync(D.d_flags + v * E, 0, E, D.stream), "memset");
             continue;
         }
-        // residue classes of this view: DB codes whose matrix rows agree on
-        // every residue of the query score identically, so the kernels may
-        // see one code per class.  Used when it lets more pair-kernel
-        // workgroups share a CU's LDS (the reference generator's uniform
-        // 28-symbol DB: '-', U, O and X score alike against a standard-residue
-        // query -> 25 classes, a 75.7 KiB table, two workgroups per CU instead
-        // of none); the class-coded residues are cached per class map.
-        std::vector<uint8_t> cls_of, cls_rep;
-        {
-            uint32_t qset = 0;
-            for (size_t i = 0; i < m; i++) qset |= 1u << (qv.seq[i] & 31);
-            cls_of.resize(D.alpha);
-            for (uint32_t c = 0; c < D.alpha; c++) {
-                const int64_t* rc = M + ((size_t)D.code_of[c] << 5);
-                size_t k = 0;
-                for (; k < cls_rep.size(); k++) {
-                    const int64_t* rk = M + ((size_t)cls_rep[k] << 5);
-                    bool same = true;
-                    for (int y = 0; y < 32 && same; y++) same = !((qset >> y) & 1) || rc[y] == rk[y];
-                    if (same) break;
-                }
-                if (k == cls_rep.size()) cls_rep.push_back(D.code_of[c]);
-                cls_of[c] = (uint8_t)k;
-            }
-        }
-        // (workgroups per CU, strip height) of the pair kernel for a compact
-        // alphabet of a codes
-        auto pair_wgs = [&](size_t a) {
-            const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1, m);
-            const size_t b = (a + 1) * (a + 1) * (pn + 4) * 4;
-            const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
-            return std::make_pair(w, pn);
-        };
-        const bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
-                             pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
+        // which kernels, bounds and strip plan (plan_view); a fused batch
+        // planned every query up front with shared bounds
+        ViewPlan vpl;
+        if (fused) vpl = fplans[v];
+        else plan_view(D, qv, nw, np, nullptr, vpl);
+        const ViewPlan& vp = vpl;
+        const bool use_cls = vp.use_cls;
+        const std::vector<uint8_t>& cls_of = vp.cls_of;
+        const std::vector<uint8_t>& cls_rep = vp.cls_rep;
         const uint4* dres = D.d_res;
         if (use_cls) {
             if (D.cls_key != cls_of) {
@@ -943,64 +1173,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             dres = D.d_res_cls;
         }
         const std::vector<uint8_t>& code_of = use_cls ? cls_rep : D.code_of;
-        // profile bounds over the residue codes the DB holds
-        const uint32_t A = (uint32_t)code_of.size();
-        int64_t minM = INT64_MAX, maxM = INT64_MIN;
-        for (size_t i = 0; i < m; i++)
-            for (uint32_t c = 0; c < A; c++) {
-                const int64_t x = M[(code_of[c] << 5) + qv.seq[i]];
-                minM = std::min(minM, x);
-                maxM = std::max(maxM, x);
-            }
-        if (A == 0) minM = maxM = 0;
-        const bool fits16 = minM >= -32768 && maxM <= 32767;
-        uint32_t nmax16 = fits16 ? (nw ? nw_int16_limit(m, Q, R, minM, maxM) : 0xffffffffu) : 0;
-        // SW with a positive gap increment (R > 0 or Q + R > 0): E would keep
-        // growing through the strip kernels' padding columns past an entry's
-        // end and leak into its maximum -- every lane goes to the exact int64
-        // kernel (the reference's full_sw recurrence)
-        if (!nw && (R > 0 || Q + R > 0)) nmax16 = 0;
-        if (C.force_wide) nmax16 = 0;
-        // SW on f16 bit patterns needs non-positive gaps and scores within
-        // +-1024 so no pattern can leave [0x0400, 0x7C7F] (kernels.hip)
-        const uint32_t prow = A + 1;
-        // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
-        const int pnp = pair_strip_np(C.pair_np, nw, prow, m);
-        const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
-        // pair kernel (diagonal-relative f16 patterns): only when no more than
-        // a handful of entries exceed its length bound (those are re-scored
-        // by the int64 kernel); otherwise the strip kernels
-        uint32_t nw_base = 0;
-        bool use_pair = false;
-        uint32_t long_groups = 0;            // leading groups scored by long_kernel
-        if (C.sw_kernel == 0 && np == 16 && pair_lds <= kPairLdsMax && nmax16 > 0) {
-            uint32_t lim = nw ? nw_f16_limit(m, Q, R, minM, maxM, &nw_base) : sw_rel_limit(m, Q, R, minM, maxM);
-            lim = std::min(lim, nmax16);
-            if (lim > 0) {
-                const size_t beyond = (size_t)(D.len_sorted.end() -
-                                               std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
-                const uint32_t lg = long_plan(D, m, beyond, Q, R, minM, maxM);
-                // (an entry beyond the bound would also corrupt its group's
-                // other lanes, whose padding columns run to its length: the
-                // group must go to long_kernel, or the strip kernels run)
-                if (lg != UINT32_MAX) {
-                    use_pair = true;
-                    nmax16 = lim;
-                    long_groups = lg == UINT32_MAX ? 0 : lg;
-                }
-            }
-        }
-        // SW on f16 patterns without the pair table (strip_f16m_kernel) needs
-        // non-positive gaps and scores within +-1024
-        const bool use_f16 = use_pair || (!nw && C.sw_kernel != 1 && Q <= 0 && R <= 0 && minM >= -1024 && maxM <= 1024);
-        // strip profile table, dword (s, c, r) = (QP[c][s*2np+r], QP[c][s*2np+np+r]);
-        // pair table of a strip of height 2P from row i0,
-        //   dword (c1*prow+c0, r) = (QP[c1][i0+r], QP[c0][i0+P+r])
-        const uint32_t nstrips = (uint32_t)((m + 2 * np - 1) / (2 * np));
-        // NW on the pair kernel is diagonal-relative: every profile value (and
-        // the padding value 0) carries -2R
-        const int rel = use_pair ? -2 * R : 0;
-        const int16_t padv = nw ? (int16_t)rel : (use_f16 ? (int16_t)(-1024 + rel) : -32768);
+        const uint32_t A = vp.A, prow = vp.prow;
+        const int64_t minM = vp.minM, maxM = vp.maxM;
+        const uint32_t nmax16 = vp.nmax16, nw_base = vp.nw_base, long_groups = vp.long_groups;
+        const int pnp = vp.pnp;
+        const size_t pair_lds = vp.pair_lds;
+        const bool use_pair = vp.use_pair, use_f16 = vp.use_f16;
+        const uint32_t nstrips = vp.nstrips;
+        const int rel = vp.rel;
+        const int16_t padv = vp.padv;
         // profile values P[c][i] (16-bit, clamped), padding rows/codes = padv;
         // rows up to the last strip's end so table builders need no bounds test
         const size_t mpad = std::max<size_t>((size_t)nstrips * 2 * np, m + 2 * pnp) + 64;
@@ -1014,28 +1195,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         auto prow_of = [&](uint32_t c) { return P.data() + (size_t)std::min(c, A) * mpad; };
         auto val = [&](uint32_t c, size_t i) -> int16_t { return (int16_t)prow_of(c)[i]; };
-        // pair kernel plan (one launch): main strips of 2*pnp rows, then a
-        // tail strip of the smallest height (multiple of 8 rows) that holds the
-        // remainder; NW always ends in a tail strip, which captures its score
         std::vector<uint32_t> qpt;
-        size_t qpt_words = 0;                // device table size (dwords)
-        uint32_t main_strips = 0;
-        int tail_np = 0;
-        size_t tail_off = 0;
-        if (use_pair) {
-            const uint32_t Hm = 2 * pnp;
-            uint32_t full = (uint32_t)(m / Hm);
-            const uint32_t rem = (uint32_t)(m % Hm);
-            if (rem > 0) {
-                tail_np = (int)(rem + 7) / 8 * 4;     // 8-row granularity
-            } else if (nw) {
-                full--;
-                tail_np = pnp;
-            }
-            main_strips = full;
-            tail_off = (size_t)full * prow * prow * pnp;
-            qpt_words = tail_off + (size_t)prow * prow * tail_np;
-        } else {
+        size_t qpt_words = vp.qpt_words;     // device table size (dwords)
+        const uint32_t main_strips = vp.main_strips;
+        const int tail_np = vp.tail_np;
+        const size_t tail_off = vp.tail_off;
+        if (!use_pair) {
             qpt.resize((size_t)nstrips * 32 * np);
             qpt_words = qpt.size();
             for (uint32_t s = 0; s < nstrips; s++)
@@ -1053,9 +1218,9 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
         // a multi-view search's earlier views may still be queued on the
         // stream: drain it before a device buffer they read is reallocated
-        if (piped && v > 0 && (D.qpt_cap < qpt_words || D.work_cap < (size_t)wide_threads * 2 * m))
+        if (piped && v > 0 && ((!fused && D.qpt_cap < qpt_words) || D.work_cap < (size_t)wide_threads * 2 * m))
             check(hipStreamSynchronize(D.stream), "sync");
-        if (D.qpt_cap < qpt_words) {
+        if (!fused && D.qpt_cap < qpt_words) {
             dfree(D.d_qpt);
             check(hipMalloc((void**)&D.d_qpt, qpt_words * 4), "qpt");
             D.qpt_cap = qpt_words;
@@ -1094,30 +1259,44 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         // view's copies may still be queued behind its predecessor's kernel
         // (waited for before the buffer is refilled or reallocated); growing
         // the device block drains the stream (its kernels read the old one)
-        if (piped && v > 0) {
-            if (D.upblk_cap < blk_bytes) check(hipStreamSynchronize(st), "sync");
-            else check(hipEventSynchronize(D.ev[5]), "staging");
+        // (a fused batch: every query its own regions, allocated up front --
+        // all of them are read by the one pair launch after the last view)
+        uint8_t* dup = D.d_upblk;
+        uint8_t* hup = D.h_up;
+        uint32_t* dqpt = D.d_qpt;
+        if (fused) {
+            dup = D.d_upblk + v * fstride;
+            hup = D.h_up + v * fstride;
+            dqpt = D.d_qpt + v * qpt_words;
+        } else {
+            if (piped && v > 0) {
+                if (D.upblk_cap < blk_bytes) check(hipStreamSynchronize(st), "sync");
+                else check(hipEventSynchronize(D.ev[5]), "staging");
+            }
+            if (D.upblk_cap < blk_bytes) {
+                dfree(D.d_upblk);
+                D.upblk_cap = blk_bytes + 4096;
+                check(hipMalloc((void**)&D.d_upblk, D.upblk_cap), "per-search uploads");
+            }
+            // one pinned staging buffer for the per-search uploads (pageable
+            // sources would make each copy a synchronous staged transfer)
+            if (D.h_up_cap < up_bytes) {
+                if (D.h_up) (void)hipHostFree(D.h_up);
+                check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
+                D.h_up_cap = up_bytes;
+            }
+            dup = D.d_upblk;
+            hup = D.h_up;
+            dqpt = D.d_qpt;
         }
-        if (D.upblk_cap < blk_bytes) {
-            dfree(D.d_upblk);
-            D.upblk_cap = blk_bytes + 4096;
-            check(hipMalloc((void**)&D.d_upblk, D.upblk_cap), "per-search uploads");
-        }
-        D.d_matrix = (int64_t*)D.d_upblk;
-        D.d_top = (uint32_t*)(D.d_upblk + kUpHeader);
-        D.d_query = D.d_upblk + kUpHeader + top_bytes;
-        // one pinned staging buffer for the per-search uploads (pageable
-        // sources would make each copy a synchronous staged transfer)
-        if (D.h_up_cap < up_bytes) {
-            if (D.h_up) (void)hipHostFree(D.h_up);
-            check(hipHostMalloc((void**)&D.h_up, up_bytes, hipHostMallocDefault), "pinned uploads");
-            D.h_up_cap = up_bytes;
-        }
+        D.d_matrix = (int64_t*)dup;
+        D.d_top = (uint32_t*)(dup + kUpHeader);
+        D.d_query = dup + kUpHeader + top_bytes;
         // staging mirrors the device block, then the strip kernels' table
-        uint8_t* up_m = D.h_up;
+        uint8_t* up_m = hup;
         uint8_t* up_t = up_m + kUpHeader;
         uint8_t* up_s = up_t + top_bytes;
-        uint8_t* up_q = D.h_up + ((blk_bytes + 15) & ~(size_t)15);
+        uint8_t* up_q = hup + ((blk_bytes + 15) & ~(size_t)15);
         memcpy(up_m, Mc, 1024 * 8);
         for (int y = 0; y < 32; y++) memcpy(up_m + 8192 + 8 * y, &M[y], 8);   // code 0's row, M[0][y]
         if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
@@ -1125,8 +1304,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
         check(hipEventRecord(D.ev[4], st), "event");
         if (!qpt.empty())
-            check(hipMemcpyAsync(D.d_qpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
-        check(hipMemcpyAsync(D.d_upblk, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
+            check(hipMemcpyAsync(dqpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+        check(hipMemcpyAsync(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
         if (piped) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
         // overflow list of this view: the whole list, or in a multi-view
         // search its own slice (all views stay on the device until the end)
@@ -1138,7 +1317,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         a.groups = D.d_groups;
         a.lane_len = D.d_lane_len;
         a.lane_out = D.d_lane_out;
-        a.qpt = D.d_qpt;
+        a.qpt = dqpt;
         a.scores = D.d_scores + (piped ? v * E : 0);
         a.ovf_list = ovf + 1;
         a.ovf_count = ovf;
@@ -1296,7 +1475,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             TableArgs ta{};
             ta.query = D.d_query;
             ta.matrix = D.d_matrix;
-            ta.out = D.d_qpt;
+            ta.out = dqpt;
             ta.m = (uint32_t)m;
             ta.alpha = A;
             ta.np = (uint32_t)pnp;
@@ -1321,7 +1500,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (use_pair) {
             StripArgs b = a;
             b.nstrips = main_strips;
-            b.qpt_tail = D.d_qpt + tail_off;
+            b.qpt_tail = dqpt + tail_off;
             b.top = (const uint4*)D.d_top;
             b.g_first = long_groups;
             if (C.pair_ticket) b.ticket = gate + 1;    // zeroed by the tables kernel just before
@@ -1334,30 +1513,47 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 const uint32_t pg = C.pair_prio_groups < 0 ? D.nsimd : (uint32_t)C.pair_prio_groups;
                 b.g_prio = (uint32_t)std::min<uint64_t>((uint64_t)long_groups + pg, D.ngroups);
             }
+            // a fused batch: view 0's arguments plus per-query strides cover
+            // every view, launched once after the last view's tables
+            if (fused && v == 0) fb = b;
+            if (fused && v + 1 == V) {
+                b = fb;
+                b.nq = (uint32_t)V;
+                for (size_t i = 0; i < V; i++) b.qm[i] = (uint32_t)views[i].len;
+                b.q_tab_stride = qpt_words;
+                b.q_score_stride = E;
+                b.q_ovf_stride = ovf_capv + 1;
+                if (main_strips + (tail_np > 0 ? 1u : 0u) > 1) {
+                    b.rowbuf = (uint4*)D.d_rowbuf_q;
+                    b.q_rowbuf_stride = (size_t)D.nblocks * 256;
+                }
+                b.timeline = nullptr;
+            }
             // strip parts: the launch's last work units become a fraction of a
             // group (kernels.h StripArgs::nparts)
-            {
+            if (!fused || v + 1 == V) {
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
+                const size_t nqf = fused ? V : 1;
                 uint32_t parts = C.pair_parts > 0 ? (uint32_t)C.pair_parts : 1u;
                 parts = std::min(parts, T);
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
                     const uint32_t ps = (T + parts - 1) / parts;
                     parts = (T + ps - 1) / ps;
-                    if (D.part_cap < quads || D.smax_cap < (size_t)D.ngroups * 64) {
+                    if (D.part_cap < quads * nqf || D.smax_cap < (size_t)D.ngroups * 64 * nqf) {
                         if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
-                        if (D.part_cap < quads) {
+                        if (D.part_cap < quads * nqf) {
                             dfree(D.d_part);
-                            check(hipMalloc((void**)&D.d_part, (size_t)quads * 4), "strip parts");
-                            D.part_cap = quads;
+                            check(hipMalloc((void**)&D.d_part, (size_t)quads * nqf * 4), "strip parts");
+                            D.part_cap = quads * nqf;
                         }
-                        if (D.smax_cap < (size_t)D.ngroups * 64) {
+                        if (D.smax_cap < (size_t)D.ngroups * 64 * nqf) {
                             dfree(D.d_smax);
-                            check(hipMalloc((void**)&D.d_smax, (size_t)D.ngroups * 64 * 4), "strip-part maxima");
-                            D.smax_cap = (size_t)D.ngroups * 64;
+                            check(hipMalloc((void**)&D.d_smax, (size_t)D.ngroups * 64 * nqf * 4), "strip-part maxima");
+                            D.smax_cap = (size_t)D.ngroups * 64 * nqf;
                         }
                     }
-                    check(hipMemsetAsync(D.d_part, 0, (size_t)quads * 4, st), "memset");
+                    check(hipMemsetAsync(D.d_part, 0, (size_t)quads * nqf * 4, st), "memset");
                     b.nparts = parts;
                     b.part_strips = ps;
                     b.nquads = quads;
@@ -1368,121 +1564,134 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
             }
             const int lnp = main_strips ? pnp : tail_np;
-            check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
+            if (!fused || v + 1 == V)
+                check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
-        if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
-        if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
-        check(hipEventRecord(ev_k1, st), "event");
-        check(launch_wide(w, wide_threads, st), "wide kernel launch");
-        if (want_counts) {
-            // 8/16-bit overflow flags of this view's lanes (counters.hip);
-            // "ordinary" widths are decided from exact values and bounds
-            int64_t lo = minM, hi = maxM, pm = INT64_MIN;
-            for (size_t i = 0; i < m; i++) {
-                const int64_t x = M[qv.seq[i]];           // padding code 0
-                lo = std::min(lo, x);
-                hi = std::max(hi, x);
-                pm = std::max(pm, x);
-            }
-            int ordinary = 0;
-            for (int b = 0; b < 2; b++) {
-                const int64_t imin = b ? -32768 : -128, imax = b ? 32767 : 127;
-                const bool ok = Q <= 0 && R <= 0 && Q + R >= imin && (!nw || Q + R <= -1) && lo >= imin && hi <= imax;
-                ordinary |= (int)ok << b;
-            }
-            FlagArgs fa{};
-            fa.res = dres;
-            fa.groups = D.d_groups;
-            fa.lane_len = D.d_lane_len;
-            fa.lane_out = D.d_lane_out;
-            fa.entry_lane = (const uint2*)D.d_entry_lane;
-            fa.entries = (uint32_t)E;
-            fa.scores = a.scores;
-            fa.query = D.d_query;
-            fa.matrix = D.d_matrix;
-            fa.padrow = (const int64_t*)(D.d_upblk + 8192);
-            fa.flags = D.d_flags + v * E;
-            fa.list = D.d_flist;
-            fa.work = (int32_t*)D.d_work;
-            fa.nlanes = D.ngroups * 64;
-            fa.m = (uint32_t)m;
-            fa.threads = wide_threads;
-            fa.gap_open = Q;
-            fa.gap_extend = R;
-            fa.nw = nw ? 1 : 0;
-            fa.widths = bw == BIT_WIDTH_8 ? 3 : 2;
-            fa.ordinary = ordinary;
-            fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
-            fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
-            if (nw && long_groups > 0 && long_hmm) {
-                fa.hmm = D.d_hmm;
-                fa.hmm_lanes = long_groups * 64;
-            }
-            fa.long_lanes = long_groups * 64;
-            fa.bw = bw;
-            fa.lists_zeroed = 1;                       // by the wide kernel just before
-            // a single view (or a batch query): counted as decided, no flags
-            // array and no count pass
-            if (ind || V == 1) fa.direct = D.d_cnt + (ind ? 2 * v : 0);
-            // pair kernel (nw_f16_limit) and int16 strip kernel (nw_int16_limit):
-            // every H of an exactly scored lane stays below 32767
-            fa.nw_hmax16_ok = nw && (use_pair || !use_f16) && nmax16 > 0 ? 1 : 0;
-            if (nw && D.ngroups > 0) {
-                // row-major NW replay: scratch for the longest entry's
-                // columns, 64..1024 lanes within 64 MiB
-                fa.rstride = D.group_ncols[0];
-                fa.rthreads = (uint32_t)std::max<size_t>(64, std::min<size_t>(1024, (64ull << 20) / (8ull * fa.rstride)) / 64 * 64);
-                const size_t need = (size_t)fa.rthreads * 2 * fa.rstride;
-                if (D.frwork_cap < need) {
-                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
-                    dfree(D.d_frwork);
-                    check(hipMalloc((void**)&D.d_frwork, need * 4), "row-major replay scratch");
-                    D.frwork_cap = need;
+        // what follows the DP kernels for this view: the exact re-score, the
+        // overflow flags, its filter pass (a fused batch defers it until the
+        // one pair launch that covers every view)
+        auto post = [=, &D, &kernel_bytes, &counted]() {
+            if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
+            if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
+            check(hipEventRecord(ev_k1, st), "event");
+            check(launch_wide(w, wide_threads, st), "wide kernel launch");
+            if (want_counts) {
+                // 8/16-bit overflow flags of this view's lanes (counters.hip);
+                // "ordinary" widths are decided from exact values and bounds
+                int64_t lo = minM, hi = maxM, pm = INT64_MIN;
+                for (size_t i = 0; i < m; i++) {
+                    const int64_t x = M[qv.seq[i]];           // padding code 0
+                    lo = std::min(lo, x);
+                    hi = std::max(hi, x);
+                    pm = std::max(pm, x);
                 }
-                fa.rlist = D.d_frlist;
-                fa.rwork = D.d_frwork;
+                int ordinary = 0;
+                for (int b = 0; b < 2; b++) {
+                    const int64_t imin = b ? -32768 : -128, imax = b ? 32767 : 127;
+                    const bool ok = Q <= 0 && R <= 0 && Q + R >= imin && (!nw || Q + R <= -1) && lo >= imin && hi <= imax;
+                    ordinary |= (int)ok << b;
+                }
+                FlagArgs fa{};
+                fa.res = dres;
+                fa.groups = D.d_groups;
+                fa.lane_len = D.d_lane_len;
+                fa.lane_out = D.d_lane_out;
+                fa.entry_lane = (const uint2*)D.d_entry_lane;
+                fa.entries = (uint32_t)E;
+                fa.scores = a.scores;
+                fa.query = D.d_query;
+                fa.matrix = D.d_matrix;
+                fa.padrow = (const int64_t*)(dup + 8192);
+                fa.flags = D.d_flags + v * E;
+                fa.list = D.d_flist;
+                fa.work = (int32_t*)D.d_work;
+                fa.nlanes = D.ngroups * 64;
+                fa.m = (uint32_t)m;
+                fa.threads = wide_threads;
+                fa.gap_open = Q;
+                fa.gap_extend = R;
+                fa.nw = nw ? 1 : 0;
+                fa.widths = bw == BIT_WIDTH_8 ? 3 : 2;
+                fa.ordinary = ordinary;
+                fa.maxm = (int32_t)std::max<int64_t>(0, std::min<int64_t>(hi, INT32_MAX));
+                fa.padmax = (int32_t)std::max<int64_t>(0, std::min<int64_t>(pm, INT32_MAX));
+                if (nw && long_groups > 0 && long_hmm) {
+                    fa.hmm = D.d_hmm;
+                    fa.hmm_lanes = long_groups * 64;
+                }
+                fa.long_lanes = long_groups * 64;
+                fa.bw = bw;
+                fa.lists_zeroed = 1;                       // by the wide kernel just before
+                // a single view (or a batch query): counted as decided, no flags
+                // array and no count pass
+                if (ind || V == 1) fa.direct = D.d_cnt + (ind ? 2 * v : 0);
+                // pair kernel (nw_f16_limit) and int16 strip kernel (nw_int16_limit):
+                // every H of an exactly scored lane stays below 32767
+                fa.nw_hmax16_ok = nw && (use_pair || !use_f16) && nmax16 > 0 ? 1 : 0;
+                if (nw && D.ngroups > 0) {
+                    // row-major NW replay: scratch for the longest entry's
+                    // columns, 64..1024 lanes within 64 MiB
+                    fa.rstride = D.group_ncols[0];
+                    fa.rthreads = (uint32_t)std::max<size_t>(64, std::min<size_t>(1024, (64ull << 20) / (8ull * fa.rstride)) / 64 * 64);
+                    const size_t need = (size_t)fa.rthreads * 2 * fa.rstride;
+                    if (D.frwork_cap < need) {
+                        if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                        dfree(D.d_frwork);
+                        check(hipMalloc((void**)&D.d_frwork, need * 4), "row-major replay scratch");
+                        D.frwork_cap = need;
+                    }
+                    fa.rlist = D.d_frlist;
+                    fa.rwork = D.d_frwork;
+                }
+                check(launch_flags(fa, st), "overflow flags launch");
+                if (!fa.direct && v + 1 == V) {
+                    // the search's counters over all views
+                    CountArgs ca{};
+                    ca.flags = D.d_flags;
+                    ca.entries = (uint32_t)E;
+                    ca.views = (uint32_t)V;
+                    ca.bw = bw;
+                    ca.out = D.d_cnt;
+                    check(launch_count(ca, st), "overflow count launch");
+                }
+                if (v + 1 == V) {
+                    check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st), "D2H counters");
+                    counted = true;
+                }
             }
-            check(launch_flags(fa, st), "overflow flags launch");
-            if (!fa.direct && v + 1 == V) {
-                // the search's counters over all views
-                CountArgs ca{};
-                ca.flags = D.d_flags;
-                ca.entries = (uint32_t)E;
-                ca.views = (uint32_t)V;
-                ca.bw = bw;
-                ca.out = D.d_cnt;
-                check(launch_count(ca, st), "overflow count launch");
+            kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
+            if (ind) {
+                // this query's own filter pass into its own candidate region
+                uint32_t* reg = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
+                FilterArgs f{};
+                f.scores = D.d_scores + v * E;
+                f.order = nullptr;
+                f.n = (uint32_t)E;
+                f.k = (uint32_t)k;
+                f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
+                f.summary = D.d_summary;
+                f.thresh = D.d_thresh;
+                f.thresh_local = D.d_thresh_local;
+                f.before = D.d_before;
+                f.ovf_count = ovf;
+                f.ovf_stride = 0;
+                f.nviews = 1;
+                f.counters = reg;
+                f.cand = (uint2*)(reg + kFilterHeader);
+                check(launch_filter(f, st), "filter launch");
+                check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
+                                     hipMemcpyDeviceToHost, st), "D2H candidates");
             }
-            if (v + 1 == V) {
-                check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st), "D2H counters");
-                counted = true;
-            }
+        };
+        if (fused && v + 1 < V) {
+            deferred.push_back(post);
+            continue;
         }
-        kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
-        if (ind) {
-            // this query's own filter pass into its own candidate region
-            uint32_t* reg = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
-            FilterArgs f{};
-            f.scores = D.d_scores + v * E;
-            f.order = nullptr;
-            f.n = (uint32_t)E;
-            f.k = (uint32_t)k;
-            f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
-            f.summary = D.d_summary;
-            f.thresh = D.d_thresh;
-            f.thresh_local = D.d_thresh_local;
-            f.before = D.d_before;
-            f.ovf_count = ovf;
-            f.ovf_stride = 0;
-            f.nviews = 1;
-            f.counters = reg;
-            f.cand = (uint2*)(reg + kFilterHeader);
-            check(launch_filter(f, st), "filter launch");
-            check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
-                                 hipMemcpyDeviceToHost, st), "D2H candidates");
-        }
+        for (auto& f : deferred) f();
+        deferred.clear();
+        post();
         if (piped && v + 1 < V) continue;
         check(hipEventRecord(D.ev[2], st), "event");
         if (ind) {
@@ -1612,7 +1821,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             take_wide(v, D.h_ovf[0], out, v);
         }
         float t;
-        if (piped) {
+        if (fused) {
+            // one launch for all views: from the first view's start to its end
+            check(hipEventElapsedTime(&t, D.vev[0], D.vev[2 * V - 1]), "elapsed");
+            kms += t;
+            for (size_t vv = 0; vv < V; vv++) (*indep)[vv].kernel_ms = t / V;
+        } else if (piped) {
             for (size_t vv = 0; vv < V; vv++) {
                 check(hipEventElapsedTime(&t, D.vev[2 * vv], D.vev[2 * vv + 1]), "elapsed");
                 kms += t;
@@ -1658,6 +1872,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.kernel_bytes = kernel_bytes;
     out.kernel = kname;
     out.strip_rows = srows;
+    out.fused_views = fused ? (uint32_t)V : 0u;
 }
 
 }  // namespace ssa

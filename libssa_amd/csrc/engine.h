@@ -99,6 +99,9 @@ struct DeviceDB {
     size_t part_cap = 0;
     uint32_t* d_smax = nullptr;
     size_t smax_cap = 0;
+    // fused batches (StripArgs::nq): one row buffer per query
+    uint8_t* d_rowbuf_q = nullptr;
+    size_t rowbuf_q_cap = 0;
     // long entries (long_kernel, launched on stream_long beside the pair
     // kernel): the groups' column counts (longest first), their sum, the
     // device's SIMD count, the multi-pass scratch
@@ -159,6 +162,7 @@ struct SearchScores {
     uint64_t wide_count = 0, kernel_bytes = 0;
     const char* kernel = "";
     uint32_t strip_rows = 0;             // pair kernel main strip height
+    uint32_t fused_views = 0;            // views one fused pair_kernel launch scored (0: not fused)
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;

@@ -10,6 +10,8 @@ constexpr int kPairWaves = 4;      // waves per pair_kernel workgroup (they shar
 constexpr size_t kPairLdsMax = 160 * 1024;  // pair table budget: one workgroup per CU (49 KiB for 20-letter proteins: 3)
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
+constexpr int kMaxFuse = 8;        // queries one pair_kernel launch may score (StripArgs::nq)
+
 struct GroupDesc {
     uint32_t blk;     // residue offset in 1 KiB blocks (16 columns x 64 lanes)
     uint32_t ncols;   // columns to compute: multiple of 4, >= longest + 1 (blocks: ceil(ncols/16))
@@ -69,6 +71,15 @@ struct StripArgs {
     uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)
     uint32_t* part_smax;       // [ngroups * 64]
     uint32_t* part_err;        // set when a wait timed out (the host then refuses the result)
+    // pair_kernel: several queries of one plan in one launch (a batch of
+    // short queries, ssa_amd_search_batch): unit order part, quad (longest
+    // first), query; query qi reads its tables at qpt / qpt_tail + qi *
+    // q_tab_stride and writes scores / overflow list / row buffer at the
+    // strides below.  Parts and strip counts are the same for every query;
+    // its row count is qm[qi].  nq 0/1: one query (a.m).
+    uint32_t nq;
+    uint32_t qm[kMaxFuse];
+    size_t q_tab_stride, q_score_stride, q_ovf_stride, q_rowbuf_stride;
 };
 
 // Long DB entries (long_kernel): the query rows split over the lanes of W

@@ -519,6 +519,14 @@ pair_kernel(const StripArgs a) {
         __syncthreads();
         wg = __builtin_amdgcn_readfirstlane(lds[0]);
     }
+    // several queries (StripArgs::nq): unit = (part, quad, query), query innermost
+    const uint32_t nq = a.nq > 1 ? a.nq : 1u;
+    uint32_t qi = 0;
+    if (nq > 1) {
+        const uint32_t u = wg;
+        wg = u / nq;
+        qi = u - wg * nq;
+    }
     // strip parts (StripArgs::nparts): unit wg = part `part` of quad wg
     uint32_t part = 0;
     if (a.nparts > 1) {
@@ -531,7 +539,8 @@ pair_kernel(const StripArgs a) {
             // ends (bounded anyway -- a timeout is reported, never a hang)
             if (threadIdx.x == 0) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(a.part_done + wg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < part) {
+                while (__hip_atomic_load(a.part_done + (size_t)wg * nq + qi, __ATOMIC_ACQUIRE,
+                                         __HIP_MEMORY_SCOPE_AGENT) < part) {
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {       // 0.5 s
                         __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -549,11 +558,26 @@ pair_kernel(const StripArgs a) {
     const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     const uint32_t gg = active ? g : a.g_first;
 
+    // this unit's query: rows, tables, outputs
+    // (a select chain: a dynamic index into the by-value argument block
+    // would copy it to scratch; qi is wave-uniform, so these are SALU selects)
+    uint32_t m = a.m;
+    if (nq > 1) {
+        m = a.qm[0];
+#pragma unroll
+        for (int k = 1; k < kMaxFuse; k++) m = qi == (uint32_t)k ? a.qm[k] : m;
+    }
+    const uint32_t* const qpt = a.qpt + qi * a.q_tab_stride;
+    const uint32_t* const qpt_tail = a.qpt_tail + qi * a.q_tab_stride;
+    int32_t* const scores = a.scores + qi * a.q_score_stride;
+    uint32_t* const ovf_list = a.ovf_list + qi * a.q_ovf_stride;
+    uint32_t* const ovf_count = a.ovf_count + qi * a.q_ovf_stride;
+
     const GroupDesc gd = a.groups[gg];
     const uint32_t nquads = gd.ncols >> 2;
     const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
-    uint4* rbp = a.rowbuf + (size_t)gd.blk * 256 + lane;
+    uint4* rbp = a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane;
     const uint32_t gl = gg * 64 + lane;
     const uint32_t prow = a.alpha + 1;
     const uint32_t len = a.lane_len[gl];
@@ -568,7 +592,8 @@ pair_kernel(const StripArgs a) {
     // an exact H_max + (-|R|) unless it is 0 (then the lane is re-scored)
     const uint32_t Rabs = (uint32_t)(-R);
     const uint32_t cRabs = Rabs * 0x10001u;
-    uint32_t S = (!NW && part > 0 && active) ? a.part_smax[gl] : 0u;
+    uint32_t* const smax = a.part_smax + (size_t)qi * a.ngroups * 64;
+    uint32_t S = (!NW && part > 0 && active) ? smax[gl] : 0u;
     // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
     uint32_t cap = 0;
     int cap_half = 0;
@@ -591,8 +616,8 @@ pair_kernel(const StripArgs a) {
         if (!active) return;
         const bool first = (i0 == 0);
         // the last strip's boundary row has no reader
-        const bool keep = i0 + 2 * NPS < (int)a.m;
-        const int rr = (int)a.m - 1 - i0;        // strip row of the last query row (CAPS)
+        const bool keep = i0 + 2 * NPS < (int)m;
+        const int rr = (int)m - 1 - i0;          // strip row of the last query row (CAPS)
         if (CAPS) cap_half = rr >= NPS ? 1 : 0;
         const int cap_row = rr - cap_half * NPS;
         const uint32_t cap_col = len - 1 + cap_half;
@@ -835,18 +860,19 @@ pair_kernel(const StripArgs a) {
     const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
     const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
     for (uint32_t s = s0; s < min(s1, a.nstrips); s++)
-        strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, a.qpt + (size_t)s * prow * prow * NP);
+        strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, qpt + (size_t)s * prow * prow * NP);
     if (NPT > 0 && s1 == T)
-        strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, a.qpt_tail);
+        strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, qpt_tail);
 
     if (a.nparts > 1 && part + 1 < a.nparts) {
         // hand the group on: running maxima, then (after every wave's row
         // buffer stores and maxima are visible at agent scope) the part count
-        if (!NW && active) a.part_smax[gl] = S;
+        if (!NW && active) smax[gl] = S;
         __threadfence();
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(a.part_done + wg, part + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.part_done + (size_t)wg * nq + qi, part + 1, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     if (!active) return;
@@ -855,7 +881,7 @@ pair_kernel(const StripArgs a) {
     const uint32_t o = a.lane_out[gl];
     if (o == 0xffffffffu) return;
     if (len == 0) {
-        a.scores[o] = NW ? (int32_t)(a.gap_open + (int64_t)a.m * a.gap_extend) : 0;
+        scores[o] = NW ? (int32_t)(a.gap_open + (int64_t)m * a.gap_extend) : 0;
         return;
     }
     int32_t score;
@@ -868,14 +894,14 @@ pair_kernel(const StripArgs a) {
         score = (int32_t)smax + (int32_t)Rabs;
     } else {
         // back from the diagonal-relative value: + (i + j) R at (m-1, len-1)
-        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE + ((int32_t)a.m + (int32_t)len - 2) * R;
+        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE + ((int32_t)m + (int32_t)len - 2) * R;
     }
     if (ovf) {
-        const uint32_t idx = atomicAdd(a.ovf_count, 1u);
-        if (idx < a.ovf_cap) a.ovf_list[idx] = gl;
-        a.scores[o] = INT32_MIN;
+        const uint32_t idx = atomicAdd(ovf_count, 1u);
+        if (idx < a.ovf_cap) ovf_list[idx] = gl;
+        scores[o] = INT32_MIN;
     } else {
-        a.scores[o] = score;
+        scores[o] = score;
     }
 }
 
@@ -1639,7 +1665,8 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     constexpr int W = pair_waves(NP, NW);
     const uint32_t quads = (a.ngroups - a.g_first + W - 1) / W;
     if (a.nparts > 1 && a.nquads != quads) return hipErrorInvalidValue;
-    const uint32_t blocks = quads * std::max(a.nparts, 1u);
+    if (a.nq > (uint32_t)kMaxFuse) return hipErrorInvalidValue;
+    const uint32_t blocks = quads * std::max(a.nparts, 1u) * std::max(a.nq, 1u);
     hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }

@@ -1107,6 +1107,53 @@ def test_search_batch_pipelined_sub_batches():
     S.free_sequence(qb)
 
 
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_search_batch_fused_launch(algo):
+    """A sub-batch whose queries share one pair-kernel plan (strip heights and
+    counts) is scored by ONE pair_kernel launch over all of them (stats
+    kernel_launches = 1 per sub-batch): one-strip queries (no row buffer),
+    multi-strip ones (a row buffer per query), with strip parts, with the
+    longest group on long_kernel per query, k = 1..64.  Every query's result
+    equals its own sw_align / nw_align and the unfused batch's."""
+    rng = np.random.default_rng(31 + algo)
+    codes, off = syn.protein_db(6000, 23 + algo, lo=1, hi=900)
+    lens = np.diff(off).astype(np.int64)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        try:
+            for qlens, opts in (([30] * 8, {}), ([97, 104, 100, 99, 101, 98, 103, 102], {}),
+                                ([97, 104, 100, 99, 101, 98, 103, 102], {"pair_parts": 2}),
+                                ([30, 29, 31, 28, 27, 26, 30, 32], {"long_groups": 1}),
+                                ([5] * 3, {})):
+                qs = [S.init_sequence_fasta(S.READ_FROM_STRING,
+                                            syn.query_string(syn.protein_query(n, int(rng.integers(1 << 30)))))
+                      for n in qlens]
+                for k, v in opts.items():
+                    S.set_option(k, v)
+                for k in (1, 10, 64):
+                    exp = [[(h["score"], h["id"]) for h in fn(q, k, 16)] for q in qs]
+                    S.set_option("batch_fuse", 0)
+                    assert S.search_batch(qs, algo, k) == exp, (qlens, opts, k, "unfused")
+                    assert S.stats()["kernel_launches"] == len(qs)
+                    S.set_option("batch_fuse", 1)
+                    got = S.search_batch(qs, algo, k)
+                    assert got == exp, (qlens, opts, k)
+                    # NW with long_kernel groups and counters keeps one launch per query
+                    unfusable = algo == S.NW and "long_groups" in opts
+                    assert S.stats()["kernel_launches"] == (len(qs) if unfusable else 1), (qlens, opts)
+                S.set_option("pair_parts", 1)
+                S.set_option("long_groups", -1)
+                for q in qs:
+                    S.free_sequence(q)
+        finally:
+            S.set_option("batch_fuse", 1)
+            S.set_option("pair_parts", 1)
+            S.set_option("long_groups", -1)
+    assert lens.max() > 0
+
+
 CLI = os.path.join(os.path.dirname(po.__file__), "_ref", "libssa_example_amd")
 
 
