@@ -1534,7 +1534,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (!fused || v + 1 == V) {
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 const size_t nqf = fused ? V : 1;
-                uint32_t parts = C.pair_parts > 0 ? (uint32_t)C.pair_parts : 1u;
+                // (at most two: kernels.hip store_row's coherence argument)
+                uint32_t parts = C.pair_parts > 1 ? 2u : 1u;
                 parts = std::min(parts, T);
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;

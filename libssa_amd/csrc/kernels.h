@@ -60,12 +60,13 @@ struct StripArgs {
     // `part_strips` strips (the tail strip counts as one), run as separate
     // work units: unit u = part (u / nquads) of quad (u % nquads), so the
     // units of all groups' first parts come first (longest groups first),
-    // then all second parts, ...  A part waits until its group's previous
-    // part is done (part_done[quad], release/acquire at agent scope: the
-    // strip boundary rows cross workgroups, maybe XCDs); the SW running
-    // maximum travels in part_smax (one dword per lane).  The launch's last
-    // units are then the shortest groups' last parts -- a fraction of a
-    // whole group's work -- so the SIMDs drain together.
+    // then all second parts.  A part waits until its group's previous part
+    // is done (part_done[quad]); the strip boundary rows cross workgroups,
+    // maybe XCDs, through device-scope stores (kernels.hip store_row, whose
+    // coherence argument limits nparts to 2); the SW running maximum travels
+    // in part_smax (one dword per lane).  The launch's last units are then
+    // the shortest groups' second parts -- a fraction of a whole group's work
+    // -- so the SIMDs drain closer together.
     // nparts 1: whole groups, no carry.
     uint32_t nparts, part_strips, nquads;
     uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)

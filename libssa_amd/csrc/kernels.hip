@@ -502,6 +502,27 @@ __device__ inline uint32_t hw_place() {
     return (xcc & 0xffu) << 16 | (id & 0xffffu);
 }
 
+// Row-buffer stores of a strip-parts launch (StripArgs::nparts) are
+// device-scope: two relaxed agent-scope 64-bit atomics, i.e. plain global
+// stores carrying the device coherence bit (sc1, write-through past this
+// XCD's L2), instead of cache-wide writeback/invalidate fences (those
+// stalled every XCD: -3 % on C2).  Why that suffices for two parts: part 0
+// runs on XCD A, part 1 on XCD B; A's stores reach memory before part 1
+// starts (the flag follows a vmcnt(0) wait), A's L2 holds no dirty row-buffer
+// line that could later be written back over B's rows, and neither B's L2
+// nor its CU's L1 ever held this group's rows before (no stale copy).  With
+// three or more parts a later part could meet its own XCD's stale copy, so
+// the host never asks for more than two.
+__device__ __forceinline__ void store_row(uint4* p, uint4 v, bool dev) {
+    if (dev) {
+        uint64_t* q = (uint64_t*)p;
+        __hip_atomic_store(q, (uint64_t)v.x | (uint64_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, (uint64_t)v.z | (uint64_t)v.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *p = v;
+    }
+}
+
 template <int NP, bool NW, int NPT>
 __global__ void __launch_bounds__(64 * pair_waves(NP, NW), pair_occupancy(NP, NW))
 pair_kernel(const StripArgs a) {
@@ -520,12 +541,12 @@ pair_kernel(const StripArgs a) {
         wg = __builtin_amdgcn_readfirstlane(lds[0]);
     }
     // several queries (StripArgs::nq): unit = (part, quad, query), query innermost
-    const uint32_t nq = a.nq > 1 ? a.nq : 1u;
+    const uint32_t nqs = a.nq > 1 ? a.nq : 1u;
     uint32_t qi = 0;
-    if (nq > 1) {
+    if (nqs > 1) {
         const uint32_t u = wg;
-        wg = u / nq;
-        qi = u - wg * nq;
+        wg = u / nqs;
+        qi = u - wg * nqs;
     }
     // strip parts (StripArgs::nparts): unit wg = part `part` of quad wg
     uint32_t part = 0;
@@ -539,7 +560,7 @@ pair_kernel(const StripArgs a) {
             // ends (bounded anyway -- a timeout is reported, never a hang)
             if (threadIdx.x == 0) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(a.part_done + (size_t)wg * nq + qi, __ATOMIC_ACQUIRE,
+                while (__hip_atomic_load(a.part_done + (size_t)wg * nqs + qi, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) < part) {
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {       // 0.5 s
                         __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -549,7 +570,6 @@ pair_kernel(const StripArgs a) {
                 }
             }
             __syncthreads();
-            __threadfence();
         }
     }
     const uint32_t g = a.g_first + wg * W + wave;
@@ -562,7 +582,7 @@ pair_kernel(const StripArgs a) {
     // (a select chain: a dynamic index into the by-value argument block
     // would copy it to scratch; qi is wave-uniform, so these are SALU selects)
     uint32_t m = a.m;
-    if (nq > 1) {
+    if (nqs > 1) {
         m = a.qm[0];
 #pragma unroll
         for (int k = 1; k < kMaxFuse; k++) m = qi == (uint32_t)k ? a.qm[k] : m;
@@ -593,7 +613,11 @@ pair_kernel(const StripArgs a) {
     const uint32_t Rabs = (uint32_t)(-R);
     const uint32_t cRabs = Rabs * 0x10001u;
     uint32_t* const smax = a.part_smax + (size_t)qi * a.ngroups * 64;
-    uint32_t S = (!NW && part > 0 && active) ? smax[gl] : 0u;
+    uint32_t S = (!NW && part > 0 && active) ? __hip_atomic_load(smax + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : 0u;
+    // strip parts hand a group's boundary rows between workgroups, maybe on
+    // other XCDs (whose L2s are not coherent with this one's): store_row
+    const bool dev_out = a.nparts > 1;
     // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
     uint32_t cap = 0;
     int cap_half = 0;
@@ -821,7 +845,8 @@ pair_kernel(const StripArgs a) {
                     if (b != 0 || k != 0) {
                         ob[(k + 3) & 3] = perm(F, H[NPS - 1], SEL_LO_BHI_HI_AHI);
                         if ((k & 3) == 0 && keep)
-                            rbp[(size_t)(b * 4 + (k >> 2) - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                            store_row(rbp + (size_t)(b * 4 + (k >> 2) - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]),
+                                      dev_out);
                     }
                     if (CAPS && j >= cmin && j <= cmax) {
                         uint32_t hsel = H[0];
@@ -834,7 +859,7 @@ pair_kernel(const StripArgs a) {
             }
         }
         ob[3] = FL;
-        if (keep) rbp[(size_t)(nquads - 1) * 64] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        if (keep) store_row(rbp + (size_t)(nquads - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]), dev_out);
         if (AD) {
             // drain after the last column J = ncols-1: the odd local rows'
             // cells of column J, and each group's anti-diagonals J+1 ..
@@ -867,11 +892,12 @@ pair_kernel(const StripArgs a) {
     if (a.nparts > 1 && part + 1 < a.nparts) {
         // hand the group on: running maxima, then (after every wave's row
         // buffer stores and maxima are visible at agent scope) the part count
-        if (!NW && active) smax[gl] = S;
-        __threadfence();
+        if (!NW && active) __hip_atomic_store(smax + gl, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every wave's device-scope stores complete, then one flag store
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(a.part_done + (size_t)wg * nq + qi, part + 1, __ATOMIC_RELEASE,
+            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, part + 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         return;
     }

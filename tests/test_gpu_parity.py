@@ -361,9 +361,8 @@ def test_strip_parts_keep_scores(algo, qlen):
     """pair_kernel with each group's strips split into dependent work units
     (option "pair_parts": all groups' first parts, then the second, ...; the
     strip boundary rows and SW running maxima cross workgroups): every score
-    equals the oracle's for 2, 3 and one part per strip (more parts than
-    strips clamp), with and without long_kernel groups and start-order
-    tickets."""
+    equals the oracle's with two parts (more are clamped to two), with and
+    without long_kernel groups and start-order tickets."""
     rng = np.random.default_rng(qlen)
     q = syn.protein_query(qlen, 77 + qlen)
     lens = np.array([3000, 2800, 2600, 0, 1] + list(rng.integers(1, 500, 3000)), dtype=np.int64)
@@ -379,7 +378,7 @@ def test_strip_parts_keep_scores(algo, qlen):
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
         try:
-            for parts, lg, ticket in ((2, -1, 1), (3, 0, 1), (50, 1, 1), (3, 2, 0), (1, -1, 1)):
+            for parts, lg, ticket in ((2, -1, 1), (2, 0, 1), (50, 1, 1), (2, 2, 0), (1, -1, 1)):
                 S.set_option("pair_parts", parts)
                 S.set_option("long_groups", lg)
                 S.set_option("pair_ticket", ticket)
@@ -1125,7 +1124,7 @@ def test_search_batch_fused_launch(algo):
         try:
             for qlens, opts in (([30] * 8, {}), ([97, 104, 100, 99, 101, 98, 103, 102], {}),
                                 ([97, 104, 100, 99, 101, 98, 103, 102], {"pair_parts": 2}),
-                                ([30, 29, 31, 28, 27, 26, 30, 32], {"long_groups": 1}),
+                                ([30, 29, 31, 28, 27, 26, 30, 25], {"long_groups": 1}),
                                 ([5] * 3, {})):
                 qs = [S.init_sequence_fasta(S.READ_FROM_STRING,
                                             syn.query_string(syn.protein_query(n, int(rng.integers(1 << 30)))))
