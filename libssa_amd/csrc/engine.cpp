@@ -964,8 +964,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     float upload = 0;
     bool all_rows = V > 0;
     for (const auto& qv : views) all_rows = all_rows && qv.len > 0;
-    out.sparse = V <= (size_t)kFilterMaxViews && k > 0 && k <= (size_t)kFilterMaxK && E > 0 && all_rows &&
-                 !cfg().no_filter;
+    // (a batch runs one filter pass per query; one pass over several views
+    // covers at most kFilterMaxViews)
+    out.sparse = (indep != nullptr || V <= (size_t)kFilterMaxViews) && k > 0 && k <= (size_t)kFilterMaxK && E > 0 &&
+                 all_rows && !cfg().no_filter;
     // several views: enqueued back to back (host preparation of view v+1
     // overlaps view v on the GPU), each into its own score and overflow
     // slice, then one filter pass over all (view, entry) scores in the
@@ -1059,6 +1061,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     std::vector<ViewPlan> fplans;
     size_t fstride = 0;                  // per-query upload block / staging stride
     StripArgs fb{};                      // view 0's pair-kernel arguments
+    size_t qm_off0 = 0;                  // the row counts' offset in view 0's upload block
     std::vector<std::function<void()>> deferred;
     if (ind && V > 1 && V <= (size_t)kMaxFuse && C.batch_fuse && !C.timeline && E > 0) {
         fplans.resize(V);
@@ -1090,7 +1093,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         if (fused) {
             const size_t ncols_max = ((size_t)(D.len_sorted.empty() ? 0 : D.len_sorted.back()) + 1 + 3) & ~(size_t)3;
             const size_t top_bytes = (std::max<size_t>(ncols_max, 4) * 4 + 15) & ~(size_t)15;
-            fstride = (kUpHeader + top_bytes + mmax + 16 + 255) & ~(size_t)255;
+            fstride = (kUpHeader + top_bytes + mmax + 16 + 4 * V + 255) & ~(size_t)255;
             const size_t qw = fplans[0].qpt_words;
             const bool rows_cross = fplans[0].main_strips + (fplans[0].tail_np > 0 ? 1u : 0u) > 1;
             const size_t rb = rows_cross ? V * (size_t)D.nblocks * 4096 : 0;
@@ -1252,8 +1255,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             }
         }
         // device upload block: [matrix 8 KB][top boundary][query codes]
+        // (+ a fused batch's row counts, view 0: StripArgs::qm)
         const size_t top_bytes = (top.size() * 4 + 15) & ~(size_t)15;
-        const size_t blk_bytes = kUpHeader + top_bytes + m;
+        const size_t qm_off = (kUpHeader + top_bytes + m + 3) & ~(size_t)3;
+        const size_t blk_bytes = (fused && v == 0) ? qm_off + 4 * V : kUpHeader + top_bytes + m;
         const size_t up_bytes = blk_bytes + 16 + qpt.size() * 4;
         // the staging buffer is reused: in a multi-view search the previous
         // view's copies may still be queued behind its predecessor's kernel
@@ -1301,6 +1306,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         for (int y = 0; y < 32; y++) memcpy(up_m + 8192 + 8 * y, &M[y], 8);   // code 0's row, M[0][y]
         if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_s, qv.seq, m);
+        if (fused && v == 0)
+            for (size_t i = 0; i < V; i++) {
+                const uint32_t mi = (uint32_t)views[i].len;
+                memcpy(up_m + qm_off + 4 * i, &mi, 4);
+            }
         if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
         check(hipEventRecord(D.ev[4], st), "event");
         if (!qpt.empty())
@@ -1515,11 +1525,14 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             }
             // a fused batch: view 0's arguments plus per-query strides cover
             // every view, launched once after the last view's tables
-            if (fused && v == 0) fb = b;
+            if (fused && v == 0) {
+                fb = b;
+                qm_off0 = qm_off;
+            }
             if (fused && v + 1 == V) {
                 b = fb;
                 b.nq = (uint32_t)V;
-                for (size_t i = 0; i < V; i++) b.qm[i] = (uint32_t)views[i].len;
+                b.qm = (const uint32_t*)(D.d_upblk + qm_off0);
                 b.q_tab_stride = qpt_words;
                 b.q_score_stride = E;
                 b.q_ovf_stride = ovf_capv + 1;

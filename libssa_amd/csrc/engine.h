@@ -179,7 +179,8 @@ struct SearchScores {
 void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out,
                    std::vector<SearchScores>* indep = nullptr);
 bool batch_pipelinable(size_t nqueries, size_t k);
-constexpr size_t kMaxBatchPipe = 8;     // queries per pipelined sub-batch
+constexpr size_t kMaxBatchPipe = 16;    // queries per pipelined sub-batch (one fused launch when their plans agree)
+static_assert(kMaxBatchPipe == (size_t)kMaxFuse, "a sub-batch fuses into one pair_kernel launch");
 
 ssa_amd_stats_t& stats();
 void check(hipError_t e, const char* what);

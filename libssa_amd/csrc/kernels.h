@@ -10,7 +10,7 @@ constexpr int kPairWaves = 4;      // waves per pair_kernel workgroup (they shar
 constexpr size_t kPairLdsMax = 160 * 1024;  // pair table budget: one workgroup per CU (49 KiB for 20-letter proteins: 3)
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
-constexpr int kMaxFuse = 8;        // queries one pair_kernel launch may score (StripArgs::nq)
+constexpr int kMaxFuse = 16;       // queries one pair_kernel launch may score (StripArgs::nq)
 
 struct GroupDesc {
     uint32_t blk;     // residue offset in 1 KiB blocks (16 columns x 64 lanes)
@@ -77,9 +77,11 @@ struct StripArgs {
     // first), query; query qi reads its tables at qpt / qpt_tail + qi *
     // q_tab_stride and writes scores / overflow list / row buffer at the
     // strides below.  Parts and strip counts are the same for every query;
-    // its row count is qm[qi].  nq 0/1: one query (a.m).
+    // its row count is qm[qi] (device memory: a select chain over an array
+    // in the argument block measured 2.5 % slower on C2 -- register
+    // allocation).  nq 0/1: one query (a.m).
     uint32_t nq;
-    uint32_t qm[kMaxFuse];
+    const uint32_t* qm;
     size_t q_tab_stride, q_score_stride, q_ovf_stride, q_rowbuf_stride;
 };
 

@@ -579,14 +579,7 @@ pair_kernel(const StripArgs a) {
     const uint32_t gg = active ? g : a.g_first;
 
     // this unit's query: rows, tables, outputs
-    // (a select chain: a dynamic index into the by-value argument block
-    // would copy it to scratch; qi is wave-uniform, so these are SALU selects)
-    uint32_t m = a.m;
-    if (nqs > 1) {
-        m = a.qm[0];
-#pragma unroll
-        for (int k = 1; k < kMaxFuse; k++) m = qi == (uint32_t)k ? a.qm[k] : m;
-    }
+    const uint32_t m = nqs > 1 ? a.qm[qi] : a.m;
     const uint32_t* const qpt = a.qpt + qi * a.q_tab_stride;
     const uint32_t* const qpt_tail = a.qpt_tail + qi * a.q_tab_stride;
     int32_t* const scores = a.scores + qi * a.q_score_stride;

@@ -1076,7 +1076,7 @@ def test_search_batch_matches_single_queries():
 
 
 def test_search_batch_pipelined_sub_batches():
-    """Batches beyond one pipelined sub-batch (8 queries), every k up to the
+    """Batches beyond one pipelined sub-batch (16 queries), every k up to the
     device filter's 64, a lone last query, and overflowing queries (int64
     re-score inside a pipelined batch) -- each equal to its single search."""
     codes, off = syn.protein_db(4000, 22, lo=1, hi=700)
