@@ -41,8 +41,8 @@ struct Config {
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
     int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
-    int pair_parts = 1;                   // pair_kernel: each group's strips in N dependent parts (StripArgs::nparts),
-                                          // 1 whole groups, 0 auto
+    int pair_parts = 0;                   // pair_kernel: each group's strips in 2 dependent parts (StripArgs::nparts):
+                                          // 0 auto (groups of >= 6 strips), 1 whole groups, 2 always
     int batch_fuse = 1;                   // ssa_amd_search_batch: queries of one pair-kernel plan in one launch
     int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)

@@ -370,6 +370,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         dalloc((void**)&D.d_before, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter scan");
         dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
         dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
+        D.filter_blocks_cap = std::max<size_t>(nb, 1);
         D.h_cand_cap = 4096;
         check(hipHostMalloc((void**)&D.h_fbuf, kFilterHeader * 4 + D.h_cand_cap * 8, hipHostMallocDefault), "pinned");
     }
@@ -1028,6 +1029,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
             check(hipMalloc((void**)&D.d_thresh, nb * 4), "filter thresholds");
             D.filter_cap = V * E;
+            D.filter_blocks_cap = nb;
         }
         // insertion order (replay() in api.cpp): ID chunks of chunk_size,
         // views outer inside a chunk, entries in ID order
@@ -1124,6 +1126,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                     dfree(D.d_rowbuf_q);
                     check(hipMalloc((void**)&D.d_rowbuf_q, rb), "per-query row buffers");
                     D.rowbuf_q_cap = rb;
+                }
+                // one filter pass over every query (FilterArgs::nq): a scratch
+                // slice per query
+                const size_t nb = V * ((E + kFilterBlock - 1) / kFilterBlock);
+                if (D.filter_blocks_cap < nb) {
+                    dfree(D.d_summary); dfree(D.d_before); dfree(D.d_thresh_local); dfree(D.d_thresh);
+                    check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 4), "filter summaries");
+                    check(hipMalloc((void**)&D.d_before, nb * kFilterMaxK * 4), "filter scan");
+                    check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
+                    check(hipMalloc((void**)&D.d_thresh, nb * 4), "filter thresholds");
+                    D.filter_blocks_cap = nb;
+                    D.filter_cap = std::min(D.filter_cap, nb * kFilterBlock);
                 }
             }
         }
@@ -1547,8 +1561,13 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (!fused || v + 1 == V) {
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 const size_t nqf = fused ? V : 1;
-                // (at most two: kernels.hip store_row's coherence argument)
-                uint32_t parts = C.pair_parts > 1 ? 2u : 1u;
+                // (at most two: kernels.hip store_row's coherence argument).
+                // Auto: two parts for groups of at least 6 strips -- C2 (9)
+                // +1.9 %, C3 (13) +2.1 %, the reference's benchmark shape (11)
+                // +12 %; for 2-3 strips the handoff costs more than the drain
+                // gains (q = 64: -9 %, q = 100: -3.5 %;
+                // profiles/r03/parts_sweep.txt)
+                uint32_t parts = C.pair_parts == 0 ? (T >= 6 ? 2u : 1u) : (C.pair_parts > 1 ? 2u : 1u);
                 parts = std::min(parts, T);
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
@@ -1676,7 +1695,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
             }
             kernel_bytes += D.meta.residues + 4ull * E + qpt_words * 4;
-            if (ind) {
+            if (ind && !fused) {
                 // this query's own filter pass into its own candidate region
                 uint32_t* reg = (uint32_t*)((uint8_t*)D.d_fbuf + v * dreg);
                 FilterArgs f{};
@@ -1706,6 +1725,33 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         for (auto& f : deferred) f();
         deferred.clear();
         post();
+        if (fused) {
+            // every query's filter pass in one (FilterArgs::nq), then each
+            // query's candidates back into its pinned region
+            FilterArgs f{};
+            f.scores = D.d_scores;
+            f.n = (uint32_t)E;
+            f.k = (uint32_t)k;
+            f.nblocks = (uint32_t)((E + kFilterBlock - 1) / kFilterBlock);
+            f.summary = D.d_summary;
+            f.thresh = D.d_thresh;
+            f.thresh_local = D.d_thresh_local;
+            f.before = D.d_before;
+            f.ovf_count = D.d_ovf;
+            f.ovf_stride = 0;
+            f.nviews = 1;
+            f.counters = (uint32_t*)D.d_fbuf;
+            f.cand = (uint2*)(f.counters + kFilterHeader);
+            f.nq = (uint32_t)V;
+            f.q_scores = E;
+            f.q_ovf = ovf_capv + 1;
+            f.q_counters = dreg / 4;
+            check(launch_filter(f, st), "filter launch");
+            for (size_t vv = 0; vv < V; vv++)
+                check(hipMemcpyAsync((uint8_t*)D.h_fbuf + vv * hreg, (uint8_t*)D.d_fbuf + vv * dreg,
+                                     kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E), hipMemcpyDeviceToHost, st),
+                      "D2H candidates");
+        }
         if (piped && v + 1 < V) continue;
         check(hipEventRecord(D.ev[2], st), "event");
         if (ind) {

@@ -61,6 +61,7 @@ struct DeviceDB {
     size_t qpt_cap = 0;
     size_t scores_cap = 0;                // d_scores entries
     size_t filter_cap = 0;                // entries the filter buffers cover
+    size_t filter_blocks_cap = 0;         // 4096-entry blocks the filter scratch covers
     // multi-view searches: insertion order of (view, entry) scores for the
     // device filter (search_64.c:44-56 chunk interleave), device and host
     uint32_t* d_order = nullptr;

@@ -158,6 +158,12 @@ struct FilterArgs {
                                // (one host copy fetches everything)
     uint2* cand;               // [n] (insertion position, score) of the candidates, unordered;
                                // at counters + kFilterHeader
+    // several independent queries in one pass (a fused batch): blockIdx.y =
+    // query q reads scores + q * q_scores and ovf_count + q * q_ovf, writes
+    // counters (and cand) + q * q_counters, and uses the q-th nblocks-sized
+    // slice of the scratch arrays.  nq 0/1: one.
+    uint32_t nq;
+    size_t q_scores, q_ovf, q_counters;
 };
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 

@@ -1029,7 +1029,25 @@ __device__ __forceinline__ int32_t insert_desc(int32_t run, int32_t x, int lane,
 constexpr int kMini = 64;
 constexpr int kMinisPerBlock = kFilterBlock / kMini;   // 64
 
-__global__ void __launch_bounds__(256) filter_block(const FilterArgs a) {
+// this block's query of a batched pass (FilterArgs::nq): its slices
+__device__ __forceinline__ FilterArgs filter_query(const FilterArgs& a0) {
+    FilterArgs a = a0;
+    const uint32_t q = blockIdx.y;
+    if (q > 0) {
+        a.scores += q * a.q_scores;
+        a.ovf_count += q * a.q_ovf;
+        a.counters += q * a.q_counters;
+        a.cand = (uint2*)(a.counters + kFilterHeader);
+        a.summary += (size_t)q * a.nblocks * kFilterMaxK;
+        a.before += (size_t)q * a.nblocks * kFilterMaxK;
+        a.thresh += (size_t)q * a.nblocks;
+        a.thresh_local += (size_t)q * a.nblocks * 64;
+    }
+    return a;
+}
+
+__global__ void __launch_bounds__(256) filter_block(const FilterArgs a0) {
+    const FilterArgs a = filter_query(a0);
     __shared__ int32_t mini_max[kMinisPerBlock];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * kFilterBlock;
@@ -1073,7 +1091,8 @@ __device__ __forceinline__ int32_t merge_topk(int32_t x, int32_t y, int lane, in
 // carry-in into the stored states.  T[b] = k-th largest of all mini maxima
 // of blocks < b.
 constexpr int kPrefixWaves = 16;
-__global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterArgs a) {
+__global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterArgs a0) {
+    const FilterArgs a = filter_query(a0);
     __shared__ int32_t carry[kPrefixWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = (int)a.k;
@@ -1108,7 +1127,8 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
     }
 }
 
-__global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
+__global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
+    const FilterArgs a = filter_query(a0);
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     if (e < a.nviews) a.counters[3 + e] = a.ovf_count[(size_t)e * a.ovf_stride];
     if (e >= a.n) return;
@@ -1122,9 +1142,10 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a) {
 
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(filter_block, dim3(a.nblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(filter_prefix, dim3(1), dim3(64 * kPrefixWaves), 0, st, a);
-    hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+    const uint32_t nq = a.nq > 1 ? a.nq : 1u;
+    hipLaunchKernelGGL(filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+    hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256, nq), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -389,7 +389,7 @@ def test_strip_parts_keep_scores(algo, qlen):
                 fn = S.sw_align if algo == S.SW else S.nw_align
                 assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, keep.astype(np.uint64), 10)
         finally:
-            S.set_option("pair_parts", 1)
+            S.set_option("pair_parts", 0)
             S.set_option("long_groups", -1)
             S.set_option("pair_ticket", 1)
         S.free_sequence(qq)
@@ -1142,13 +1142,13 @@ def test_search_batch_fused_launch(algo):
                     # NW with long_kernel groups and counters keeps one launch per query
                     unfusable = algo == S.NW and "long_groups" in opts
                     assert S.stats()["kernel_launches"] == (len(qs) if unfusable else 1), (qlens, opts)
-                S.set_option("pair_parts", 1)
+                S.set_option("pair_parts", 0)
                 S.set_option("long_groups", -1)
                 for q in qs:
                     S.free_sequence(q)
         finally:
             S.set_option("batch_fuse", 1)
-            S.set_option("pair_parts", 1)
+            S.set_option("pair_parts", 0)
             S.set_option("long_groups", -1)
     assert lens.max() > 0
 

@@ -26,8 +26,12 @@ def main():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--algo", default="sw", choices=["sw", "nw"])
+    p.add_argument("--option", action="append", default=[], help="name=value passed to ssa_amd_set_option")
     args = p.parse_args()
     S.load()
+    for o in args.option:
+        k, v = o.split("=")
+        S.set_option(k, int(v))
     S.set_output_mode(S.OUTPUT_ERROR)
     S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
     nw = args.algo == "nw"
@@ -60,7 +64,7 @@ def main():
             launches = S.stats()["kernel_launches"]
         assert bat == unf == [[(s, i) for s, i in x] for x in one]
         cells = float(off[-1]) * qlen * args.nq
-        print(json.dumps({"algo": args.algo, "qlen": qlen, "nq": args.nq,
+        print(json.dumps({"algo": args.algo, "qlen": qlen, "nq": args.nq, "options": args.option,
                           "one_by_one_gcups": round(cells / min(t_one) / 1e9, 1),
                           "batch_unfused_gcups": round(cells / min(t_unf) / 1e9, 1),
                           "batch_fused_gcups": round(cells / min(t_batch) / 1e9, 1),
