@@ -99,7 +99,7 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "pair_parts" 0|1|2   pair-kernel groups run as 2 dependent work units of consecutive
  *                        strips (all groups' first parts, then all second parts),
  *                        so the launch ends on small units: 0 (default) for groups of
- *                        at least 6 strips, 1 never, 2 always
+ *                        at least 4 strips, 1 never, 2 always
  *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
  *                        m_run's INFO line): -1 (default) only at output mode
  *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always

@@ -42,7 +42,7 @@ struct Config {
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
     int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
     int pair_parts = 0;                   // pair_kernel: each group's strips in 2 dependent parts (StripArgs::nparts):
-                                          // 0 auto (groups of >= 6 strips), 1 whole groups, 2 always
+                                          // 0 auto (groups of >= 4 strips), 1 whole groups, 2 always
     int batch_fuse = 1;                   // ssa_amd_search_batch: queries of one pair-kernel plan in one launch
     int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)

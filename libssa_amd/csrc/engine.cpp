@@ -59,6 +59,8 @@ void DeviceDB::release() {
     dfree(d_rowbuf_q);
     d_rowbuf_q = nullptr;
     rowbuf_q_cap = 0;
+    dfree(d_rowbuf2);
+    d_rowbuf2 = nullptr;
     dfree(d_timeline);
     d_timeline = nullptr;
     timeline_cap = timeline_rows = 0;
@@ -718,6 +720,17 @@ static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
     return 24;
 }
 
+// strip parts of a pair-kernel launch of T strips (StripArgs::nparts; at
+// most two: kernels.hip store_row's coherence argument).  Auto: two parts for
+// groups of at least 4 strips -- C2 (9 strips) +1.1 %, C3 (13) +1.1 %, the
+// reference's benchmark shape (11) +6-8 %, q = 200 (5) +1 %; q = 100 (3)
+// -2.3 % (profiles/r03/parts_sweep.txt)
+static uint32_t strip_parts(uint32_t T) {
+    const int o = cfg().pair_parts;
+    const uint32_t p = o == 0 ? (T >= 4 ? 2u : 1u) : (o > 1 ? 2u : 1u);
+    return std::min(p, T);
+}
+
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
                           uint32_t scale = 1) {
     const Config& C = cfg();
@@ -1097,8 +1110,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             const size_t top_bytes = (std::max<size_t>(ncols_max, 4) * 4 + 15) & ~(size_t)15;
             fstride = (kUpHeader + top_bytes + mmax + 16 + 4 * V + 255) & ~(size_t)255;
             const size_t qw = fplans[0].qpt_words;
-            const bool rows_cross = fplans[0].main_strips + (fplans[0].tail_np > 0 ? 1u : 0u) > 1;
-            const size_t rb = rows_cross ? V * (size_t)D.nblocks * 4096 : 0;
+            const uint32_t T0 = fplans[0].main_strips + (fplans[0].tail_np > 0 ? 1u : 0u);
+            const bool rows_cross = T0 > 1;
+            // one row buffer per query, two with strip parts (rowbuf2 after all first ones)
+            const size_t rb = rows_cross ? V * (size_t)D.nblocks * 4096 * (strip_parts(T0) > 1 ? 2 : 1) : 0;
             if (rb > D.rowbuf_q_cap) {
                 // one row buffer per query: only within a third of the free memory
                 size_t fr = 0, tot = 0;
@@ -1561,14 +1576,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (!fused || v + 1 == V) {
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 const size_t nqf = fused ? V : 1;
-                // (at most two: kernels.hip store_row's coherence argument).
-                // Auto: two parts for groups of at least 6 strips -- C2 (9)
-                // +1.9 %, C3 (13) +2.1 %, the reference's benchmark shape (11)
-                // +12 %; for 2-3 strips the handoff costs more than the drain
-                // gains (q = 64: -9 %, q = 100: -3.5 %;
-                // profiles/r03/parts_sweep.txt)
-                uint32_t parts = C.pair_parts == 0 ? (T >= 6 ? 2u : 1u) : (C.pair_parts > 1 ? 2u : 1u);
-                parts = std::min(parts, T);
+                uint32_t parts = strip_parts(T);
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
                     const uint32_t ps = (T + parts - 1) / parts;
@@ -1593,6 +1601,15 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                     b.part_done = D.d_part;
                     b.part_smax = D.d_smax;
                     b.part_err = gate + 2;
+                    if (fused) {
+                        b.rowbuf2 = (uint4*)(D.d_rowbuf_q + nqf * (size_t)D.nblocks * 4096);
+                    } else {
+                        if (!D.d_rowbuf2) {
+                            if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                            check(hipMalloc((void**)&D.d_rowbuf2, (size_t)D.nblocks * 4096), "second row buffer");
+                        }
+                        b.rowbuf2 = D.d_rowbuf2;
+                    }
                     parts_used = true;
                 }
             }

@@ -61,10 +61,11 @@ struct StripArgs {
     // work units: unit u = part (u / nquads) of quad (u % nquads), so the
     // units of all groups' first parts come first (longest groups first),
     // then all second parts.  A part waits until its group's previous part
-    // is done (part_done[quad]); the strip boundary rows cross workgroups,
-    // maybe XCDs, through device-scope stores (kernels.hip store_row, whose
-    // coherence argument limits nparts to 2); the SW running maximum travels
-    // in part_smax (one dword per lane).  The launch's last units are then
+    // is done (part_done[quad]); the handoff boundary crosses workgroups,
+    // maybe XCDs, through device-scope stores, and part 1 keeps its own
+    // boundaries in rowbuf2 (kernels.hip store_row: the coherence argument,
+    // which limits nparts to 2); the SW running maximum travels in
+    // part_smax (one dword per lane).  The launch's last units are then
     // the shortest groups' second parts -- a fraction of a whole group's work
     // -- so the SIMDs drain closer together.
     // nparts 1: whole groups, no carry.
@@ -72,6 +73,7 @@ struct StripArgs {
     uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)
     uint32_t* part_smax;       // [ngroups * 64]
     uint32_t* part_err;        // set when a wait timed out (the host then refuses the result)
+    uint4* rowbuf2;            // part 1's own strip boundaries (same layout as rowbuf)
     // pair_kernel: several queries of one plan in one launch (a batch of
     // short queries, ssa_amd_search_batch): unit order part, quad (longest
     // first), query; query qi reads its tables at qpt / qpt_tail + qi *

@@ -502,22 +502,23 @@ __device__ inline uint32_t hw_place() {
     return (xcc & 0xffu) << 16 | (id & 0xffffu);
 }
 
-// Row-buffer stores of a strip-parts launch (StripArgs::nparts) are
-// device-scope: two relaxed agent-scope 64-bit atomics, i.e. plain global
-// stores carrying the device coherence bit (sc1, write-through past this
-// XCD's L2), instead of cache-wide writeback/invalidate fences (those
-// stalled every XCD: -3 % on C2).  Why that suffices for two parts: part 0
-// runs on XCD A, part 1 on XCD B; A's stores reach memory before part 1
-// starts (the flag follows a vmcnt(0) wait), A's L2 holds no dirty row-buffer
-// line that could later be written back over B's rows, and neither B's L2
-// nor its CU's L1 ever held this group's rows before (no stale copy).  With
-// three or more parts a later part could meet its own XCD's stale copy, so
-// the host never asks for more than two.
-__device__ __forceinline__ void store_row(uint4* p, uint4 v, bool dev) {
+// Strip parts (StripArgs::nparts = 2) hand a group's boundary rows from the
+// workgroup of part 0 (XCD A) to that of part 1 (maybe XCD B; the XCDs' L2s
+// are not coherent).  Part 0 keeps its strip boundaries in the row buffer as
+// usual, but writes its LAST boundary -- the one part 1 reads -- with
+// device-scope 16-byte stores (a buffer store with the sc1 bit: write-through
+// past A's L2, full lines), then waits for them (vmcnt 0) before the flag.
+// Part 1 reads that boundary with ordinary loads (B's L1/L2 never held these
+// lines in this kernel: dispatch invalidates them) and keeps its own
+// boundaries in a second row buffer (StripArgs::rowbuf2), so no dirty line
+// of the first buffer left in A's L2 can ever be written back over newer
+// data.  No cache-wide writeback/invalidate (those stalled every XCD: -3 %
+// on C2); the row-buffer traffic is unchanged.  Two parts at most.
+__device__ __forceinline__ void store_row(uint4* p, uint4 v, bool dev, __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
     if (dev) {
-        uint64_t* q = (uint64_t*)p;
-        __hip_atomic_store(q, (uint64_t)v.x | (uint64_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, (uint64_t)v.z | (uint64_t)v.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u x = {v.x, v.y, v.z, v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, 0, 16 /* sc1 */);
     } else {
         *p = v;
     }
@@ -590,7 +591,17 @@ pair_kernel(const StripArgs a) {
     const uint32_t nquads = gd.ncols >> 2;
     const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
-    uint4* rbp = a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane;
+    // row buffers: rb0 (part 0, and every strip without parts), rb1 (part
+    // 1's own boundaries); rbr / rbw: where the current strip reads its top
+    // boundary and writes its bottom one
+    uint4* const rb0 = a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane;
+    uint4* const rb1 = a.nparts > 1 ? a.rowbuf2 + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane : rb0;
+    uint4* rbr = rb0;
+    uint4* rbw = part > 0 ? rb1 : rb0;
+    // the handoff strip's device-scope stores (part 0's last strip)
+    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256), 0, 0x7fffffff, 0x00020000);
+    bool handoff = false;
     const uint32_t gl = gg * 64 + lane;
     const uint32_t prow = a.alpha + 1;
     const uint32_t len = a.lane_len[gl];
@@ -608,9 +619,7 @@ pair_kernel(const StripArgs a) {
     uint32_t* const smax = a.part_smax + (size_t)qi * a.ngroups * 64;
     uint32_t S = (!NW && part > 0 && active) ? __hip_atomic_load(smax + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                              : 0u;
-    // strip parts hand a group's boundary rows between workgroups, maybe on
-    // other XCDs (whose L2s are not coherent with this one's): store_row
-    const bool dev_out = a.nparts > 1;
+
     // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
     uint32_t cap = 0;
     int cap_half = 0;
@@ -684,7 +693,7 @@ pair_kernel(const StripArgs a) {
         // the boundary row above the strip: the previous strip's row buffer,
         // or for the first strip the lane-independent top boundary a.top
         // (a broadcast read; no per-column select between the two)
-        const uint4* qsrc = first ? a.top : rbp;
+        const uint4* qsrc = first ? a.top : rbr;
         const uint32_t qstride = first ? 1 : 64;
 
         // SW, anti-diagonal maxima (AD): cells (r, j) and (r+1, j-1) have the
@@ -838,8 +847,8 @@ pair_kernel(const StripArgs a) {
                     if (b != 0 || k != 0) {
                         ob[(k + 3) & 3] = perm(F, H[NPS - 1], SEL_LO_BHI_HI_AHI);
                         if ((k & 3) == 0 && keep)
-                            store_row(rbp + (size_t)(b * 4 + (k >> 2) - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]),
-                                      dev_out);
+                            store_row(rbw + (size_t)(b * 4 + (k >> 2) - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]),
+                                      handoff, rs0, ((b * 4 + (k >> 2) - 1) * 64 + lane) * 16);
                     }
                     if (CAPS && j >= cmin && j <= cmax) {
                         uint32_t hsel = H[0];
@@ -852,7 +861,12 @@ pair_kernel(const StripArgs a) {
             }
         }
         ob[3] = FL;
-        if (keep) store_row(rbp + (size_t)(nquads - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]), dev_out);
+        if (keep)
+            store_row(rbw + (size_t)(nquads - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]), handoff, rs0,
+                      ((nquads - 1) * 64 + lane) * 16);
+        // the next strip reads what this one wrote (part 1 after its first
+        // strip: its own buffer)
+        rbr = rbw;
         if (AD) {
             // drain after the last column J = ncols-1: the odd local rows'
             // cells of column J, and each group's anti-diagonals J+1 ..
@@ -877,16 +891,21 @@ pair_kernel(const StripArgs a) {
     const uint32_t T = a.nstrips + (NPT > 0 ? 1u : 0u);
     const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
     const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
-    for (uint32_t s = s0; s < min(s1, a.nstrips); s++)
+    for (uint32_t s = s0; s < min(s1, a.nstrips); s++) {
+        handoff = a.nparts > 1 && part == 0 && s + 1 == s1;
         strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, qpt + (size_t)s * prow * prow * NP);
-    if (NPT > 0 && s1 == T)
+    }
+    if (NPT > 0 && s1 == T) {
+        handoff = false;
         strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, qpt_tail);
+    }
 
     if (a.nparts > 1 && part + 1 < a.nparts) {
         // hand the group on: running maxima, then (after every wave's row
         // buffer stores and maxima are visible at agent scope) the part count
         if (!NW && active) __hip_atomic_store(smax + gl, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every wave's device-scope stores complete, then one flag store
+        __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (threadIdx.x == 0)
