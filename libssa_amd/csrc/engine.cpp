@@ -1526,10 +1526,17 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.zero = ovf;
             if (C.pair_ticket) ta.zero_ticket = gate + 1;
             if (long_groups > 0) {
-                // (at most the first 512 workgroups: more may not all fit the
-                // chip at once, and the rest follow the first in order)
+                // (at most what can be resident at once: every long workgroup
+                // pads its LDS to the pair table's size, so a CU holds
+                // floor(160 KiB / that) of them -- beyond it the target is
+                // reached only as early ones retire, and the wait would run
+                // into its 20 ms bound; and at most 512, the rest follow the
+                // first in order)
+                const size_t lds_long = std::max(pair_lds, long_lds_bytes(A, 4, m <= 512 ? 2 : 4));
+                const uint32_t resident = (uint32_t)std::max<size_t>(1, kPairLdsMax / std::max<size_t>(lds_long, 1)) *
+                                          (D.nsimd / 4);
                 ta.gate = gate;
-                ta.gate_target = std::min<uint32_t>(gate_total, gate_base + 512);
+                ta.gate_target = std::min<uint32_t>(gate_total, gate_base + std::min<uint32_t>(512, resident));
             }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {
