@@ -731,6 +731,9 @@ static uint32_t strip_parts(uint32_t T) {
     return std::min(p, T);
 }
 
+// long_kernel at 4 waves per entry: rows per lane for an m-row query
+static int long_rl4(size_t m) { return m <= 512 ? 2 : m <= 768 ? 3 : 4; }
+
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
                           uint32_t scale = 1) {
     const Config& C = cfg();
@@ -1472,8 +1475,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 la.hmm = D.d_hmm;
                 long_hmm = true;
             }
-            const int rl4 = m <= 512 ? 2 : 4;
-            const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 768 ? 12 : 16;
+            // rows per lane: the fewest computed rows for this query (a
+            // wave of W waves x 64 lanes x RL rows per pass; waves past the
+            // query idle): q = 513 computes 576 rows at RL 3, 768 at RL 4
+            const int rl4 = long_rl4(m);
+            const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 576 ? 9 : m <= 768 ? 12 : 16;
             if (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1) {
                 la.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)long_groups * 64 * la.stride;
@@ -1532,7 +1538,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 // reached only as early ones retire, and the wait would run
                 // into its 20 ms bound; and at most 512, the rest follow the
                 // first in order)
-                const size_t lds_long = std::max(pair_lds, long_lds_bytes(A, 4, m <= 512 ? 2 : 4));
+                const size_t lds_long = std::max(pair_lds, long_lds_bytes(A, 4, long_rl4(m)));
                 const uint32_t resident = (uint32_t)std::max<size_t>(1, kPairLdsMax / std::max<size_t>(lds_long, 1)) *
                                           (D.nsimd / 4);
                 ta.gate = gate;

@@ -1296,10 +1296,14 @@ __device__ __forceinline__ int32_t shr1(int32_t lane0_value, int32_t v) {
     return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138, 0xf, 0xf, false);
 }
 
-// one lane's profile slice: RL int16 values (rows i0 .. i0+RL-1 of a code)
+// one lane's profile slice: RL int16 values (rows i0 .. i0+RL-1 of a code),
+// padded to an even count (odd RL: W * 64 * RL rows per pass fit query
+// lengths just past a power of two, e.g. P18080's 513 rows: 4 x 64 x 3 = 768
+// rows of which 576 are computed, against 768 at RL = 4)
+constexpr int rl_pad(int rl) { return (rl + 1) & ~1; }
 template <int RL>
 struct ProfSlice {
-    uint32_t v[RL / 2];
+    uint32_t v[rl_pad(RL) / 2];
 };
 
 template <int W, int RL, bool NW, bool TRK>
@@ -1309,12 +1313,14 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     // reason as LongArgs::lds_min: a finished long wave's registers must take
     // a pair wave
     asm volatile("" ::: "v167");
-    extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][RP] profile of the pass
+    extern __shared__ __attribute__((aligned(16))) int16_t ltab[];   // [code][lane slot][RLP] profile of the pass
     __shared__ int2 ring[W > 1 ? W - 1 : 1][W > 1 ? kLongRing : 1];
     __shared__ int32_t wmax[kLongWaves], wlo[kLongWaves];
     constexpr int EPW = kLongWaves / W;              // entries per workgroup
     constexpr uint32_t RW = 64 * RL;                 // rows per wave
     constexpr uint32_t RP = W * RW;                  // rows per pass
+    constexpr uint32_t RLP = rl_pad(RL);             // profile slots per lane
+    constexpr uint32_t CS = W * 64 * RLP;            // profile table stride per code
     constexpr int PF = 2;                            // profile loads issued PF steps ahead
     // these waves are the launch's critical path: they issue before the
     // pair kernel's waves sharing their SIMD
@@ -1354,9 +1360,11 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         // fence orders the previous pass's scratch stores before its loads
         __threadfence();
         __syncthreads();
-        for (uint32_t x = threadIdx.x; x < prow * RP; x += 64 * kLongWaves) {
-            const uint32_t c = x / RP, i = i0p + x % RP;
-            ltab[x] = (c < a.alpha && i < m) ? (int16_t)a.matrix[(c << 5) + a.query[i]] : (int16_t)-4096;
+        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * kLongWaves) {
+            const uint32_t c = x / CS, rem = x % CS, sl = rem / RLP, k = rem % RLP;
+            const uint32_t i = i0p + sl * RL + k;
+            ltab[x] = (c < a.alpha && k < (uint32_t)RL && i < m) ? (int16_t)a.matrix[(c << 5) + a.query[i]]
+                                                                 : (int16_t)-4096;
         }
         __syncthreads();
         if (nmax == 0) continue;
@@ -1369,7 +1377,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         const int lmax = wact ? (int)((min(m - i0w, RW) - 1) / RL) : -1;
         const bool feeds_ring = W > 1 && wr + 1 < W && i0w + RW < m;
         const bool feeds_scratch = !lastp && wr + 1 == W;
-        const int16_t* prof = ltab + (i0 - i0p);          // + code * RP
+        const int16_t* prof = ltab + (wr * 64 + lane) * RLP;   // + code * CS
         // left boundary: H(i, -1) and E into column 0
         int32_t H[RL], E[RL], hlo[RL], hhi[RL];
 #pragma unroll
@@ -1419,7 +1427,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
                 dn_ = (w_ >> (8 * (u_ & 3))) & 0xffu;                                              \
             }                                                                                      \
             d = (uint32_t)shr1((int32_t)dn_, (int32_t)d);                                          \
-            dst = *(const ProfSlice<RL>*)(prof + d * RP);                                          \
+            dst = *(const ProfSlice<RL>*)(prof + d * CS);                                          \
         }
         auto scr_load = [&](uint32_t c) __attribute__((always_inline)) -> int64_t {
             return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -1443,8 +1451,8 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         // lane 63's last row to the next wave (ring) or pass (scratch)
 #define LONG_ROWS(pcv, hin, fin, tval)                                                            \
         {                                                                                          \
-            int32_t P_[RL];                                                                        \
-            _Pragma("unroll") for (int k_ = 0; k_ < RL / 2; k_++) {                                \
+            int32_t P_[RLP];                                                                       \
+            _Pragma("unroll") for (int k_ = 0; k_ < (int)RLP / 2; k_++) {                          \
                 P_[2 * k_] = (int32_t)(int16_t)((pcv).v[k_] & 0xffffu);                            \
                 P_[2 * k_ + 1] = (int32_t)(pcv).v[k_] >> 16;                                       \
             }                                                                                      \
@@ -1524,7 +1532,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
                     const uint32_t w_ = q_ == 0 ? b0 : q_ == 1 ? b1 : q_ == 2 ? b2 : b3;           \
                     const uint32_t dn_ = (w_ >> (8 * ((k + 2) & 3))) & 0xffu;                      \
                     d = (uint32_t)shr1((int32_t)dn_, (int32_t)d);                                  \
-                    pq1 = *(const ProfSlice<RL>*)(prof + d * RP);                                  \
+                    pq1 = *(const ProfSlice<RL>*)(prof + d * CS);                                  \
                 }                                                                                  \
                 const int32_t hin = shr1(th, hbot);                                                \
                 const int32_t fin = shr1(tf, fbot);                                                \
@@ -1645,7 +1653,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
 
 #undef LONG_ISSUE
 
-size_t long_lds_bytes(uint32_t alpha, int w, int rl) { return (size_t)(alpha + 1) * w * 64 * rl * 2; }
+size_t long_lds_bytes(uint32_t alpha, int w, int rl) { return (size_t)(alpha + 1) * w * 64 * rl_pad(rl) * 2; }
 
 template <int W, int RL, bool NW, bool TRK>
 static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
@@ -1678,6 +1686,7 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
     if (w == 4) {
         switch (rl) {
             case 2: return nw ? launch_long_t<4, 2, true>(a, st) : launch_long_t<4, 2, false>(a, st);
+            case 3: return nw ? launch_long_t<4, 3, true>(a, st) : launch_long_t<4, 3, false>(a, st);
             case 4: return nw ? launch_long_t<4, 4, true>(a, st) : launch_long_t<4, 4, false>(a, st);
             default: return hipErrorInvalidValue;
         }
@@ -1686,6 +1695,7 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
     switch (rl) {
         case 4: return nw ? launch_long_t<1, 4, true>(a, st) : launch_long_t<1, 4, false>(a, st);
         case 8: return nw ? launch_long_t<1, 8, true>(a, st) : launch_long_t<1, 8, false>(a, st);
+        case 9: return nw ? launch_long_t<1, 9, true>(a, st) : launch_long_t<1, 9, false>(a, st);
         case 12: return nw ? launch_long_t<1, 12, true>(a, st) : launch_long_t<1, 12, false>(a, st);
         case 16: return nw ? launch_long_t<1, 16, true>(a, st) : launch_long_t<1, 16, false>(a, st);
         default: return hipErrorInvalidValue;
