@@ -58,6 +58,9 @@ typedef struct {
     uint32_t strip_rows;     /* pair kernel: rows of its main strips (2 x "pair_np"); 0: other kernels */
     uint32_t counters;       /* 1: overflow_8/16 were computed (bit width 64, output mode >= OUTPUT_INFO
                                 or option "counters" 1); 0: not computed, they read 0 */
+    uint32_t long_entries;   /* lanes (64 per group) of the longest groups scored by a long-entry kernel (view 0) */
+    char long_kernel[24];    /* that kernel: "long16_rl<R>" (packed 16-bit SW), "long32_w<W>_rl<R>" (int32;
+                                "+"-joined when split over two launches), "" none */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -91,6 +94,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        for the rest), always 4, always 1
  *   "long4_share_pct" P  auto: 4 waves per entry for groups longer than P % of
  *                        one SIMD's share of all columns
+ *   "long16" 1|0         SW long entries on packed 16-bit patterns, one wave
+ *                        per entry, whenever min(m, n) x max score fits (default);
+ *                        0: the int32 kernel ("long_waves" applies to it)
  *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
  *                        wave priority: none (default), one per SIMD, N
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)

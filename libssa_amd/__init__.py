@@ -66,7 +66,8 @@ class ssa_amd_stats_t(Structure):
                 ("overflow_8", c_uint64), ("overflow_16", c_uint64), ("wide_count", c_uint64),
                 ("kernel_launches", c_uint32), ("device", c_int32), ("kernel_bytes", c_uint64),
                 ("kernel", ctypes.c_char * 32), ("prep_ms", c_double), ("upload_ms", c_double),
-                ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32)]
+                ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32),
+                ("long_entries", c_uint32), ("long_kernel", ctypes.c_char * 24)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -242,6 +243,7 @@ def stats():
     load().ssa_amd_get_stats(ctypes.byref(s))
     d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
     d["kernel"] = d["kernel"].decode()
+    d["long_kernel"] = d["long_kernel"].decode()
     return d
 
 

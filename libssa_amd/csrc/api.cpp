@@ -107,6 +107,8 @@ void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPl
     S.device = plan.empty() ? -1 : plan[0].device;
     snprintf(S.kernel, sizeof S.kernel, "%s", sc.empty() ? "" : sc[0].kernel);
     S.strip_rows = sc.empty() ? 0 : sc[0].strip_rows;
+    S.long_entries = sc.empty() ? 0 : sc[0].long_entries;
+    snprintf(S.long_kernel, sizeof S.long_kernel, "%s", sc.empty() ? "" : sc[0].long_kernel);
 }
 
 void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {
@@ -414,6 +416,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "long_share_pct")) cfg().long_share_pct = (int)value;
     else if (!strcmp(name, "long_waves")) cfg().long_waves = (int)value;
     else if (!strcmp(name, "long4_share_pct")) cfg().long4_share_pct = (int)value;
+    else if (!strcmp(name, "long16")) cfg().long16 = (int)value;
     else if (!strcmp(name, "pair_prio_groups")) cfg().pair_prio_groups = (int)value;
     else if (!strcmp(name, "timeline")) cfg().timeline = (int)value;
     else if (!strcmp(name, "pair_ticket")) cfg().pair_ticket = (int)value;

@@ -734,6 +734,23 @@ static uint32_t strip_parts(uint32_t T) {
 // long_kernel at 4 waves per entry: rows per lane for an m-row query
 static int long_rl4(size_t m) { return m <= 512 ? 2 : m <= 768 ? 3 : 4; }
 
+// long16_kernel (SW long entries on packed 16-bit patterns): the pattern of
+// score 0 -- high enough that h + Q + R and E + R never borrow across the
+// halves -- and the rows per lane for an m-row query (the fewest rows >= m
+// of 64 x {4, 6, 8, 10, 12, 16}, passes of 1024 rows beyond), or 0 when the
+// kernel does not apply: NW, the option off, or min(m, n) maxM (the largest
+// SW score) beyond the patterns' finite range (kernels.hip long16_kernel)
+static uint32_t long16_base(int Q, int R) { return 0x0400u + (uint32_t)std::max(0, -(Q + R)); }
+static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM) {
+    if (nw || !cfg().long16 || Q > 0 || R > 0 || Q + R < -16384 || minM < -32768 || D.len_sorted.empty()) return 0;
+    const int64_t mp = std::max<int64_t>(maxM, 0);
+    const int64_t hmax = (int64_t)std::min<size_t>(m, D.len_sorted.back()) * mp;
+    if ((int64_t)long16_base(Q, R) + hmax + mp > 0x7BFF) return 0;
+    for (int rl : {4, 6, 8, 10, 12})
+        if (m <= (size_t)64 * rl) return rl;
+    return 16;
+}
+
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
                           uint32_t scale = 1) {
     const Config& C = cfg();
@@ -1165,6 +1182,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     uint64_t kernel_bytes = 0;
     const char* kname = "";
     uint32_t srows = 0;
+    char lkname[24] = "";                // long-entry kernel(s) of view 0 (stats)
+    uint32_t lentries = 0;
     bool parts_used = false;                 // some view ran strip parts (their wait-timeout word is read back)
 
     for (size_t v = 0; v < V; v++) {
@@ -1422,14 +1441,18 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         check(hipEventRecord(ev_k0, st), "event");
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
+        size_t lds_long = pair_lds;   // LDS of a long workgroup (the pair tables' gate)
         if (long_groups > 0) {
+            const int rl16 = long16_plan(D, m, nw, Q, R, minM, maxM);
             // the longest groups on their own streams, concurrently with the
             // pair kernel (enqueued first, so their waves start first): one
             // wave per entry (RL rows per lane, 64*RL rows per pass), or --
             // for the groups so long that one wave's latency would outlast
             // the pair kernel -- one workgroup per entry, its rows over 4
             // waves (RL 2 up to 512 rows, else 4, passes of 1024 rows)
-            if (C.long_waves == 4) {
+            if (rl16 > 0) {
+                long4 = 0;                 // (one wave per entry)
+            } else if (C.long_waves == 4) {
                 long4 = long_groups;
             } else if (C.long_waves == 0) {
                 const double thr4 = (double)D.ncols_sum / D.nsimd * C.long4_share_pct / 100.0;
@@ -1480,7 +1503,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             // query idle): q = 513 computes 576 rows at RL 3, 768 at RL 4
             const int rl4 = long_rl4(m);
             const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 576 ? 9 : m <= 768 ? 12 : 16;
-            if (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1) {
+            if (rl16 > 0 ? m > (size_t)64 * rl16 : (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1)) {
                 la.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)long_groups * 64 * la.stride;
                 if (D.lscratch_cap < need) {
@@ -1509,9 +1532,24 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 la.nseq = (long_groups - long4) * 64;
                 gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
-                check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
+                if (rl16 > 0) {
+                    la.base16 = long16_base(Q, R);
+                    la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
+                    check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
+                } else {
+                    check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
+                }
                 check(hipEventRecord(D.ev[6], D.stream_long1), "event");
             }
+            if (v == 0) {
+                lentries = long_groups * 64;
+                if (rl16 > 0) snprintf(lkname, sizeof lkname, "long16_rl%d", rl16);
+                else if (long4 == 0) snprintf(lkname, sizeof lkname, "long32_w1_rl%d", rl1);
+                else if (long4 == long_groups) snprintf(lkname, sizeof lkname, "long32_w4_rl%d", rl4);
+                else snprintf(lkname, sizeof lkname, "long32_w4_rl%d+w1_rl%d", rl4, rl1);
+            }
+            lds_long = std::max(pair_lds, rl16 > 0 ? long16_lds_bytes(A, rl16)
+                                                   : long4 > 0 ? long_lds_bytes(A, 4, rl4) : long_lds_bytes(A, 1, rl1));
         }
         // the pair tables after the long entries' launch: long_kernel only
         // needs the uploads, so its workgroups are dispatched before the
@@ -1538,7 +1576,6 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 // reached only as early ones retire, and the wait would run
                 // into its 20 ms bound; and at most 512, the rest follow the
                 // first in order)
-                const size_t lds_long = std::max(pair_lds, long_lds_bytes(A, 4, long_rl4(m)));
                 const uint32_t resident = (uint32_t)std::max<size_t>(1, kPairLdsMax / std::max<size_t>(lds_long, 1)) *
                                           (D.nsimd / 4);
                 ta.gate = gate;
@@ -1883,6 +1920,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 if (hf[3]) take_wide(vv, hf[3], o, 0);
                 o.kernel = kname;
                 o.strip_rows = srows;
+                o.long_entries = lentries;
+                memcpy(o.long_kernel, lkname, sizeof lkname);
             }
         } else if (out.sparse) {
             const uint32_t nc = D.h_fbuf[0];
@@ -1962,6 +2001,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.kernel_bytes = kernel_bytes;
     out.kernel = kname;
     out.strip_rows = srows;
+    out.long_entries = lentries;
+    memcpy(out.long_kernel, lkname, sizeof lkname);
     out.fused_views = fused ? (uint32_t)V : 0u;
 }
 

@@ -164,6 +164,8 @@ struct SearchScores {
     uint64_t wide_count = 0, kernel_bytes = 0;
     const char* kernel = "";
     uint32_t strip_rows = 0;             // pair kernel main strip height
+    uint32_t long_entries = 0;           // entries the long-entry kernels scored (view 0)
+    char long_kernel[24] = {};           // which (ssa_amd_stats_t::long_kernel)
     uint32_t fused_views = 0;            // views one fused pair_kernel launch scored (0: not fused)
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];

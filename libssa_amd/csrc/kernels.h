@@ -114,6 +114,9 @@ struct LongArgs {
     // LDS takes a pair workgroup (allocations are contiguous: a smaller hole
     // beside the pair workgroups' would stay empty until one of those ends)
     uint32_t lds_min;
+    // long16_kernel (SW on 16-bit patterns): pattern of score 0, and the
+    // padding profile value (int16 in the low half)
+    uint32_t base16, pad16;
 };
 constexpr int kLongWaves = 4;
 
@@ -181,6 +184,10 @@ hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st);
 // w 4: 2 or 4); w * 64 * rl rows per pass
 hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st);
 size_t long_lds_bytes(uint32_t alpha, int w, int rl);
+// SW long entries on packed 16-bit patterns, one wave per entry; rl (rows
+// per lane) 4, 6, 8, 10, 12 or 16, 64*rl rows per pass
+hipError_t launch_long16(const LongArgs& a, int rl, hipStream_t st);
+size_t long16_lds_bytes(uint32_t alpha, int rl);
 
 // The reference's 8/16-bit overflow counters (counters.hip).  m_run reports
 // how many (query view, DB sequence) pairs its w-bit SIMD kernels sent on to

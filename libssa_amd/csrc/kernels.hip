@@ -1702,6 +1702,302 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
     }
 }
 
+// ------------------------------------------------- long entries, SW packed
+// long16_kernel: long_kernel's SW at one wave per entry on 16-bit patterns,
+// two rows per register -- the pair kernel's cell arithmetic (v_pk_* on f16
+// bit patterns) with long_kernel's lane-skewed wavefront.  Lane l of pass p
+// holds rows i0 = i0p + l*RL .. i0 + RL - 1 in RL/2 registers: register k
+// packs row i0 + k (low half) and row i0 + RL/2 + k (high half), and the
+// high half runs one column behind the low one (it takes H and F of row
+// i0 + RL/2 - 1 -- the last low row -- from the previous step, like the pair
+// kernel's strip halves).  So a lane's step covers columns j (low) and j - 1
+// (high), and the lanes are skewed by two columns: lane l's low half is at
+// column t - 2l at step t, taking the (H, F) pair its upper neighbour's high
+// half made at step t - 1 through one DPP shift -- the packed dword the pair
+// kernel keeps in its row buffer.  Its residue comes through a DPP chain
+// that moves one lane every two steps, and the high half's profile values
+// are the low half's of the previous step (one v_bfi_b32 per register).
+//
+// Absolute frame: value v is the pattern v + a.base16 (SW scores >= 0, so
+// every H, E, F is >= base16 >= 0x0400: E and F are clamped at the floor as
+// long_kernel clamps them at 0, exact for R <= 0).  The host
+// (engine.cpp long16_plan) checks base16 + min(m, n) maxM + maxM <= 0x7BFF,
+// so no real value or intermediate reaches the inf/NaN patterns, and picks
+// base16 >= 0x0400 - (Q + R) so h + Q + R cannot borrow across the halves.
+// Padding (rows past the query, the padding code of columns past an entry)
+// scores a.pad16 = maxM - 32767: hd + pad16 wraps to a negative f16 pattern
+// in [0x8001, 0xFC00], which every maximum drops, so a padding cell's H is
+// max(E, F) -- never above the real cells' maximum.
+//
+// Per register and step: 8.5 VALU for two cells (long_kernel: ~15 per cell).
+constexpr int long16_slot(int rl) { return ((rl / 2) + 1) & ~1; }   // dwords per lane slot (8-B aligned)
+template <int NR>
+struct PairSlice {
+    uint32_t v[(NR + 1) & ~1];
+};
+
+template <int RL>
+__global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs a) {
+    static_assert(RL % 2 == 0, "rows per lane come in register pairs");
+    asm volatile("" ::: "v167");                     // as long_kernel: a pair wave fits where it ran
+    extern __shared__ __attribute__((aligned(16))) uint32_t ptab[];   // [code][lane slot][SLW] dwords
+    constexpr int NR = RL / 2;                       // packed registers per lane
+    constexpr uint32_t SLW = long16_slot(RL);
+    constexpr uint32_t CS = 64 * SLW;                // dwords per code
+    constexpr uint32_t RP = 64 * RL;                 // rows per pass
+    constexpr int PF = 2;                            // profile loads issued PF steps ahead
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    if (a.gate && threadIdx.x == 0)
+        __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t s = blockIdx.x * kLongWaves + wave;   // one entry per wave
+    const bool active = s < a.nseq;
+    const uint32_t ss = a.seq0 + (active ? s : 0);
+    const GroupDesc gd = a.groups[ss >> 6];
+    const uint32_t n = active ? a.lane_len[ss] : 0;
+    const uint4* rp = a.res + (size_t)gd.blk * 64 + (ss & 63);
+    uint32_t* scr = (uint32_t*)(a.scratch + (size_t)ss * a.stride);   // packed (H, F) per column
+    const uint32_t BP = a.base16 * 0x10001u;
+    const int32_t QR = a.gap_open + a.gap_extend, R = a.gap_extend;
+    const uint32_t cQR = (uint32_t)(QR * 65536 + QR), cR = (uint32_t)(R * 65536 + R);
+    const uint32_t m = a.m, prow = a.alpha + 1, padc = a.alpha;
+    const uint32_t padw = (a.pad16 & 0xffffu) * 0x10001u;
+    const uint32_t npass = (m + RP - 1) / RP;
+    uint32_t S = BP;
+    uint32_t t = 0;
+    for (uint32_t p = 0; p < npass; p++) {
+        const uint32_t i0p = p * RP;
+        // the pass's profile, dword (c, l, k) = (QP[c][i0 + k], QP[c][i0 + NR + k])
+        // for lane l's i0; the fence orders the previous pass's scratch stores
+        // before this pass's loads
+        __threadfence();
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * kLongWaves) {
+            const uint32_t c = x / CS, rem = x % CS, sl = rem / SLW, k = rem % SLW;
+            uint32_t v = padw;
+            if (k < (uint32_t)NR && c < a.alpha) {
+                const uint32_t lo = i0p + sl * RL + k, hi = lo + NR;
+                const uint32_t vl = lo < m ? (uint32_t)(uint16_t)(int16_t)a.matrix[(c << 5) + a.query[lo]] : padw & 0xffffu;
+                const uint32_t vh = hi < m ? (uint32_t)(uint16_t)(int16_t)a.matrix[(c << 5) + a.query[hi]] : padw & 0xffffu;
+                v = vl | (vh << 16);
+            }
+            ptab[x] = v;
+        }
+        __syncthreads();
+        if (!active || n == 0) continue;
+        const bool lastp = p + 1 == npass;
+        // last lane holding query rows: it ends the pass's wavefront
+        const uint32_t lmax = (min(m - i0p, RP) - 1) / RL;
+        const uint32_t* prof = ptab + lane * SLW;    // + code * CS
+        // left boundary (SW: H(i, -1) = 0, E into column 0 = 0); the high
+        // halves first run a virtual column -1 whose inputs (floor, padding
+        // profile) reproduce that boundary
+        uint32_t H[NR], E[NR];
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            H[k] = BP;
+            E[k] = BP;
+        }
+        uint32_t hd0 = BP, Fprev = BP, ob = BP;
+        PairSlice<NR> pprev;
+#pragma unroll
+        for (int k = 0; k < (int)SLW; k++) pprev.v[k] = padw;
+        // residues: lane l issues the profile load of column u - 2l at issue
+        // step u (PF steps ahead of its use): lane 0 injects column u, and
+        // every lane takes its upper neighbour's column of two issues ago
+        uint32_t d0 = padc, d1 = padc;
+        uint32_t b0, b1, b2, b3, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        {
+            const uint4 v = rp[0];
+            b0 = v.x; b1 = v.y; b2 = v.z; b3 = v.w;
+            if (n > 16) {
+                const uint4 y = rp[64];
+                c0 = y.x; c1 = y.y; c2 = y.z; c3 = y.w;
+            }
+        }
+#define L16_ISSUE(u, dst)                                                                           \
+        {                                                                                          \
+            const uint32_t u_ = (u);                                                               \
+            uint32_t dn_ = padc;                                                                   \
+            if (u_ < n) {                                                                          \
+                if ((u_ & 15) == 0 && u_ > 0) {                                                    \
+                    b0 = c0; b1 = c1; b2 = c2; b3 = c3;                                            \
+                    if (u_ + 16 < n) {                                                             \
+                        const uint4 x_ = rp[(size_t)((u_ >> 4) + 1) * 64];                         \
+                        c0 = x_.x; c1 = x_.y; c2 = x_.z; c3 = x_.w;                                \
+                    }                                                                              \
+                }                                                                                  \
+                const uint32_t w_ = (u_ & 8) ? ((u_ & 4) ? b3 : b2) : ((u_ & 4) ? b1 : b0);        \
+                dn_ = (w_ >> (8 * (u_ & 3))) & 0xffu;                                              \
+            }                                                                                      \
+            const uint32_t dx_ = (uint32_t)shr1((int32_t)dn_, (int32_t)d1);                        \
+            d1 = d0;                                                                               \
+            d0 = dx_;                                                                              \
+            dst = *(const PairSlice<NR>*)(prof + dx_ * CS);                                        \
+        }
+        auto scr_load = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t {
+            return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : BP;
+        };
+        const bool from_scr = p > 0;
+        const bool feeds_scratch = !lastp;
+        uint32_t row = BP, row_next = BP;
+        PairSlice<NR> pq0, pq1;
+        if (from_scr) {
+            row = scr_load(lane & 15);
+            row_next = scr_load(16 + (lane & 15));
+        }
+        L16_ISSUE(0u, pq0);
+        L16_ISSUE(1u, pq1);
+        // lane lmax's high half finishes column n - 1 at step n - 1 + 2 lmax + 1
+        const uint32_t steps = n + 2 * lmax + 1;
+        t = 0;
+        // one step of a lane: its NR registers over columns j (low halves)
+        // and j - 1 (high halves); rbv = (H of the row above at column j,
+        // F into this lane's first row at column j)
+#define L16_ROWS(pcv, rbv)                                                                          \
+        {                                                                                          \
+            uint32_t F_ = perm(Fprev, (rbv), SEL_LO_BHI_HI_ALO);                                   \
+            uint32_t hd_ = hd0;                                                                    \
+            _Pragma("unroll") for (int k_ = 0; k_ < NR; k_++) {                                    \
+                const uint32_t P_ = ((pcv).v[k_] & 0xffffu) | (pprev.v[k_] & 0xffff0000u);         \
+                const uint32_t h_ = fmax3(padd16(hd_, P_), E[k_], F_);                             \
+                hd_ = H[k_];                                                                       \
+                H[k_] = h_;                                                                        \
+                const uint32_t tt_ = h_ + cQR;                                                     \
+                E[k_] = fmax3(E[k_] + cR, tt_, BP);                                                \
+                F_ = fmax3(F_ + cR, tt_, BP);                                                      \
+                if (k_ & 1) S = fmax3(S, H[k_ - 1], H[k_]);                                        \
+            }                                                                                      \
+            if (NR & 1) S = fmax2(S, H[NR - 1]);                                                   \
+            asm volatile("" : "+v"(S));                                                            \
+            hd0 = perm(hd_, (rbv), SEL_LO_BLO_HI_ALO);                                             \
+            Fprev = F_;                                                                            \
+            ob = perm(F_, H[NR - 1], SEL_LO_BHI_HI_AHI);                                           \
+        }
+        // 16 steps from t (t % 16 == 0, t >= 128, t + 18 <= n): every lane
+        // has started (lane 63's high half is past column -1) and lane 0's
+        // columns and residue loads are inside the entry -- no masks, no
+        // branches: lane 63's (H, F) of columns t - 127 .. t - 112 for the
+        // next pass (FEED) are rotated into lanes 15..0 of obuf and stored
+        // after the 16 steps
+#define L16_STEADY(MODE, FEED)                                                                    \
+        {                                                                                          \
+            uint32_t obuf = 0;                                                                     \
+            _Pragma("unroll") for (int k = 0; k < 16; k++) {                                       \
+                const uint32_t tk = t + k;                                                         \
+                const PairSlice<NR> pcv = pq0;                                                     \
+                pq0 = pq1;                                                                         \
+                uint32_t top = BP;                                                                 \
+                if (MODE == 1) {                                                                   \
+                    if (k == 0) {                                                                  \
+                        row = row_next;                                                            \
+                        row_next = scr_load(tk + 16 + (lane & 15));                                \
+                    }                                                                              \
+                    top = (uint32_t)__builtin_amdgcn_readlane((int32_t)row, k);                    \
+                }                                                                                  \
+                if (k == 14) {                                                                     \
+                    b0 = c0; b1 = c1; b2 = c2; b3 = c3;                                            \
+                    if (tk + 18 < n) {                                                             \
+                        const uint4 x_ = rp[(size_t)(((tk + 2) >> 4) + 1) * 64];                   \
+                        c0 = x_.x; c1 = x_.y; c2 = x_.z; c3 = x_.w;                                \
+                    }                                                                              \
+                }                                                                                  \
+                {                                                                                  \
+                    const int q_ = ((k + 2) >> 2) & 3;                                             \
+                    const uint32_t w_ = q_ == 0 ? b0 : q_ == 1 ? b1 : q_ == 2 ? b2 : b3;           \
+                    const uint32_t dn_ = (w_ >> (8 * ((k + 2) & 3))) & 0xffu;                      \
+                    const uint32_t dx_ = (uint32_t)shr1((int32_t)dn_, (int32_t)d1);                \
+                    d1 = d0;                                                                       \
+                    d0 = dx_;                                                                      \
+                    pq1 = *(const PairSlice<NR>*)(prof + dx_ * CS);                                \
+                }                                                                                  \
+                const uint32_t rbv = (uint32_t)shr1((int32_t)top, (int32_t)ob);                    \
+                L16_ROWS(pcv, rbv);                                                                \
+                pprev = pcv;                                                                       \
+                if (FEED)   /* DPP wave_ror:1 -- lane 0 takes lane 63's ob, lane l lane l-1's obuf */ \
+                    obuf = (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)(lane == 63 ? ob : obuf), 0x13c, 0xf, 0xf, false); \
+            }                                                                                      \
+            if (FEED && lane < 16)   /* lane l holds step 15 - l */                                \
+                __hip_atomic_store(scr + (t - 112u) - lane, obuf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+        }
+        while (t < steps) {
+            if ((t & 15) == 0 && t >= 128 && t + 18 <= n) {
+                if (from_scr) {
+                    if (feeds_scratch) L16_STEADY(1, true)
+                    else L16_STEADY(1, false)
+                } else {
+                    if (feeds_scratch) L16_STEADY(0, true)
+                    else L16_STEADY(0, false)
+                }
+                t += 16;
+                continue;
+            }
+            // general step (ramp-up, drain): lanes start at step 2l
+            const PairSlice<NR> pcv = pq0;
+            pq0 = pq1;
+            uint32_t top = BP;
+            if (from_scr && t < n) {
+                if ((t & 15) == 0 && t > 0) {
+                    row = row_next;
+                    row_next = scr_load(t + 16 + (lane & 15));
+                }
+                top = (uint32_t)__builtin_amdgcn_readlane((int32_t)row, t & 15);
+            }
+            L16_ISSUE(t + PF, pq1);
+            const uint32_t rbv = (uint32_t)shr1((int32_t)top, (int32_t)ob);
+            if (t >= 2u * (uint32_t)lane) L16_ROWS(pcv, rbv);
+            pprev = pcv;
+            if (feeds_scratch && lane == 63 && t - 127u < n)
+                __hip_atomic_store(scr + (t - 127u), ob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t++;
+        }
+#undef L16_STEADY
+#undef L16_ROWS
+    }
+#undef L16_ISSUE
+    // patterns order as integers (all >= base16)
+    uint32_t smax = max(S & 0xffffu, S >> 16);
+    for (int x = 32; x > 0; x >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, x));
+    if (active && lane == 0) {
+        const uint32_t o = a.lane_out[ss];
+        if (o != 0xffffffffu) a.scores[o] = (int32_t)smax - (int32_t)a.base16;
+    }
+    if (a.timeline && active && lane == 0)
+        a.timeline[ss] = make_uint4(0x80000000u | ss, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
+}
+
+size_t long16_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * long16_slot(rl) * 4; }
+
+template <int RL>
+static hipError_t launch_long16_k(const LongArgs& a, hipStream_t st) {
+    static std::atomic<uint64_t> attr{0};
+    constexpr size_t kDynMax = kPairLdsMax - 8192;
+    const size_t need = long16_lds_bytes(a.alpha, RL);
+    if (need > kDynMax) return hipErrorInvalidValue;
+    const size_t bytes = std::max<size_t>(need, std::min<size_t>(a.lds_min, kDynMax));
+    const hipError_t e = lds_attr_once((const void*)long16_kernel<RL>, attr, (int)kDynMax);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
+    hipLaunchKernelGGL((long16_kernel<RL>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_long16(const LongArgs& a, int rl, hipStream_t st) {
+    if (a.nseq == 0) return hipSuccess;
+    if (a.alpha > 32 || a.base16 < 0x0400u || a.base16 > 0x7BFFu) return hipErrorInvalidValue;
+    switch (rl) {
+        case 4: return launch_long16_k<4>(a, st);
+        case 6: return launch_long16_k<6>(a, st);
+        case 8: return launch_long16_k<8>(a, st);
+        case 10: return launch_long16_k<10>(a, st);
+        case 12: return launch_long16_k<12>(a, st);
+        case 16: return launch_long16_k<16>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 // ------------------------------------------------------------------ launch
 template <int NP, bool NW>
 static hipError_t launch_np(const StripArgs& a, hipStream_t st) {

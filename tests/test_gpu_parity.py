@@ -275,7 +275,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
         S.free_sequence(qq)
 
 
-def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None):
+def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0):
     rng = np.random.default_rng(1000 + qlen)
     q = syn.protein_query(qlen, 200 + qlen)
     head = [3000, 1, 0, 2500, 17, 64, 4100, qlen + 7] + ([35000, 22000, 20001] if huge else [])
@@ -296,6 +296,7 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None):
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
         S.set_option("long_waves", waves)
+        S.set_option("long16", long16)
         if share4 is not None:
             S.set_option("long4_share_pct", share4)
         try:
@@ -304,11 +305,18 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None):
                 sc, ids = _full_scores(qq, algo, len(keep))
                 assert (ids == keep).all()
                 assert (sc == exp).all(), (lg, np.nonzero(sc != exp)[0][:10])
+                st = S.stats()
+                if st["kernel"].startswith("pair"):
+                    assert st["long_entries"] == 64 * lg
+                    if lg:
+                        packed = long16 and algo == S.SW
+                        assert st["long_kernel"].startswith("long16" if packed else "long32"), st["long_kernel"]
                 got = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
                 assert got == po.topk(exp, keep.astype(np.uint64), 10)
         finally:
             S.set_option("long_groups", -1)
             S.set_option("long_waves", 0)
+            S.set_option("long16", 1)
             S.set_option("long4_share_pct", 400)
         S.free_sequence(qq)
 
@@ -395,17 +403,29 @@ def test_strip_parts_keep_scores(algo, qlen):
         S.free_sequence(qq)
 
 
-@pytest.mark.parametrize("qlen", [1, 5, 63, 64, 65, 255, 256, 257, 400, 512, 513, 768, 769, 1024, 1025, 1500, 2049])
+LONG_QLENS = [1, 5, 63, 64, 65, 255, 256, 257, 384, 385, 400, 512, 513, 640, 641, 768, 769, 1024, 1025, 1500, 2049]
+
+
+@pytest.mark.parametrize("qlen", LONG_QLENS)
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 @pytest.mark.parametrize("waves", [4, 1])
 def test_long_entry_kernel_vs_oracle(qlen, algo, waves):
-    """long_kernel (an entry's query rows over the lanes of 4 waves or of one,
-    passes of up to 1024 rows) on the leading (longest) groups -- forced to 1
-    and 3 of the groups, and to none -- gives every entry the oracle's score;
-    the DB has entries of 1..4100 residues, empty records and planted copies
-    of the query; with 4 waves also entries of 20-35 k residues (UniProt's
-    longest)."""
+    """long_kernel (int32; an entry's query rows over the lanes of 4 waves or
+    of one, passes of up to 1024 rows) on the leading (longest) groups --
+    forced to 1 and 3 of the groups, and to none -- gives every entry the
+    oracle's score; the DB has entries of 1..4100 residues, empty records and
+    planted copies of the query; with 4 waves also entries of 20-35 k
+    residues (UniProt's longest)."""
     _long_entry_case(qlen, algo, (-11, -1), waves, huge=waves == 4 and qlen in (5, 400, 513, 1025, 2049))
+
+
+@pytest.mark.parametrize("qlen", LONG_QLENS)
+def test_long16_kernel_vs_oracle(qlen):
+    """long16_kernel (SW on packed 16-bit patterns, two rows per register,
+    one wave per entry, rows per lane 4..16, passes of 1024 rows beyond) on the
+    same DBs: every score the oracle's, with the 20-35 k-residue entries for
+    the query lengths the benchmark configurations use."""
+    _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=qlen in (5, 400, 513, 1025, 2049), long16=1)
 
 
 @pytest.mark.parametrize("qlen", [5, 400, 1025])
@@ -422,9 +442,45 @@ def test_long_entry_kernel_split_launches(qlen, algo):
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_long_entry_kernel_gap_penalties(gaps, qlen, algo):
     """long_kernel's SW clamps E and F at 0 (exact for R <= 0) and its NW is
-    the plain recurrence: zero, steep and unequal gap penalties against the
-    oracle."""
+    the plain recurrence, as long16_kernel's SW clamps at the score-0 pattern:
+    zero, steep and unequal gap penalties against the oracle."""
     _long_entry_case(qlen, algo, gaps, 4, huge=False)
+    if algo == S.SW:
+        _long_entry_case(qlen, algo, gaps, 1, huge=False, long16=1)
+
+
+@pytest.mark.parametrize("match", [60, 102, 103, 120])
+def test_long16_score_bound(match):
+    """long16_kernel's exactness bound, base16 + min(m, n) maxM + maxM <=
+    0x7BFF (engine.cpp long16_plan): a 300-residue query on a constant
+    matrix with copies of itself planted in 2-5 k-residue entries scores
+    300 x match; match 102 still fits (base16 0x0404), 103 and up the int32
+    kernel takes the long groups -- every score exact either way."""
+    rng = np.random.default_rng(match)
+    q = rng.choice(syn.AA_CODES, size=300).astype(np.uint8)
+    lens = np.array([5000, 4200, 3000, 2500] + list(rng.integers(1, 400, 700)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    for e, at in ((0, 4000), (2, 17), (3, 2200)):
+        codes[int(off[e]) + at:int(off[e]) + at + 300] = q
+    M = po.matrix_constant(match, -1)
+    exp = po.scores(S.SW, q, codes, off, M, -3, -1)
+    assert exp.max() == 300 * match
+    configure(False, ("const", match, -1), -3, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            S.set_option("long_groups", 1)
+            sc, _ = _full_scores(qq, S.SW, len(lens))
+            assert (sc == exp).all(), np.nonzero(sc != exp)[0][:10]
+            st = S.stats()
+            if st["long_entries"]:
+                assert st["long_kernel"].startswith("long16" if match <= 102 else "long32"), st["long_kernel"]
+        finally:
+            S.set_option("long_groups", -1)
+        S.free_sequence(qq)
 
 
 @pytest.mark.parametrize("match", [40, 55, 127])
