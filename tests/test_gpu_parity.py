@@ -1569,3 +1569,4 @@ def test_short_sw_queries_take_32_row_strips():
                 assert (sc == exp_nw[keep]).all(), (m, np.nonzero(sc != exp_nw[keep])[0][:10])
                 assert S.stats()["strip_rows"] == (48 if m <= 48 else 80), m
             S.free_sequence(qq)
+

@@ -4,7 +4,11 @@ and what the launch's tail is made of.
 
 usage: python tools/timeline.py PATH.npy
 Rows: (group | 0x80000000 + lane for long_kernel, start, end, place), ticks of
-the 100 MHz s_memrealtime clock; place = XCC << 16 | HW_ID[15:0]."""
+the 100 MHz s_memrealtime clock; place = XCC << 16 | HW_ID[15:0].  With strip
+parts (option "pair_parts", auto for queries of >= 4 strips) a pair group's row
+is its LAST part's workgroup: start is when that part began (after the group's
+earlier parts), so pair "starts" late in the span -- use option pair_parts=1 to
+see whole groups."""
 import sys
 
 import numpy as np
