@@ -59,11 +59,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals),
 # pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory),
 # pmc_{c2,c3,c5,ref}_r01g (+ diagonal add as v_add_u32, long_kernel),
-# profiles/r02/pmc_c2_s3 (48-row SW strips, the default, 24-bit LDS address) and
-# profiles/r02/pmc_c3_np40 (80-row NW strips, the default).  Keyed by
+# profiles/r02/pmc_c2_s3 (48-row SW strips, the default, 24-bit LDS address),
+# profiles/r02/pmc_c3_np40 (80-row NW strips, the default) and
+# profiles/r03/pmc_c2 (round 3: strip parts, long16_kernel; 6.654e9 x 64 /
+# 1.406e11 = 3.03).  Keyed by
 # (kernel, pair strip rows): the instruction count per cell depends on the
 # strip height.
-VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 3.02,
+VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 3.03,
                        ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.66}
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
