@@ -61,6 +61,10 @@ void DeviceDB::release() {
     rowbuf_q_cap = 0;
     dfree(d_rowbuf2);
     d_rowbuf2 = nullptr;
+    dfree(d_paddr);
+    d_paddr = nullptr;
+    paddr_valid = false;
+    paddr_cls.clear();
     dfree(d_timeline);
     d_timeline = nullptr;
     timeline_cap = timeline_rows = 0;
@@ -1664,6 +1668,32 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
             }
             const int lnp = main_strips ? pnp : tail_np;
+            if (!fused || v + 1 == V) {
+                // the pair-row stream (StripArgs::paddr) for the launch's table
+                // row width, rebuilt when the residue copy, code count or row
+                // width it was made for changes (a fused batch shares view 0's
+                // plan; on this stream any earlier pair launch has finished
+                // reading it before it is rewritten)
+                const uint32_t rowB = (uint32_t)(lnp + 4) * 4;
+                if (!D.paddr_valid || D.paddr_use_cls != use_cls || D.paddr_prow != A + 1 ||
+                    D.paddr_row_bytes != rowB || (use_cls && D.paddr_cls != cls_of)) {
+                    if (!D.d_paddr) check(hipMalloc((void**)&D.d_paddr, (size_t)D.nblocks * 4096), "pair-row stream");
+                    PairAddrArgs pa{};
+                    pa.res = dres;
+                    pa.out = D.d_paddr;
+                    pa.groups = D.d_groups;
+                    pa.ngroups = D.ngroups;
+                    pa.prow = A + 1;
+                    pa.row_bytes = rowB;
+                    check(launch_pair_addr(pa, st), "pair-row stream launch");
+                    D.paddr_valid = true;
+                    D.paddr_use_cls = use_cls;
+                    D.paddr_prow = A + 1;
+                    D.paddr_row_bytes = rowB;
+                    D.paddr_cls = use_cls ? cls_of : std::vector<uint8_t>();
+                }
+                b.paddr = D.d_paddr;
+            }
             if (!fused || v + 1 == V)
                 check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {

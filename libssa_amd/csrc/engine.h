@@ -124,6 +124,13 @@ struct DeviceDB {
     // and the class map it was made with
     uint4* d_res_cls = nullptr;
     std::vector<uint8_t> cls_key;
+    // pair_kernel main strips' pair-row stream (StripArgs::paddr, as
+    // d_rowbuf) and what it was built from: residue copy (class map), code
+    // count + 1, row width
+    uint4* d_paddr = nullptr;
+    std::vector<uint8_t> paddr_cls;
+    bool paddr_valid = false, paddr_use_cls = false;
+    uint32_t paddr_prow = 0, paddr_row_bytes = 0;
     size_t rec_begin = 0, rec_end = 0;    // plugin records [rec_begin, rec_end) of this shard
     void release();
 };

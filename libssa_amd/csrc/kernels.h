@@ -85,6 +85,11 @@ struct StripArgs {
     uint32_t nq;
     const uint32_t* qm;
     size_t q_tab_stride, q_score_stride, q_ovf_stride, q_rowbuf_stride;
+    // pair_kernel: the pair-row stream (pair_addr_kernel), the LDS byte
+    // offset of each column's next pair row in row-buffer quads, built for
+    // this launch's table row width ((NP + 4) dwords, or (NPT + 4) when
+    // nstrips = 0) and code count
+    const uint4* paddr;
 };
 
 // Long DB entries (long_kernel): the query rows split over the lanes of W
@@ -259,6 +264,22 @@ struct RecodeArgs {
     uint8_t map[64];
 };
 hipError_t launch_recode(const RecodeArgs& a, hipStream_t st);
+
+// pair_kernel's strips read, per column j, the LDS byte offset of the
+// pair row of column j+1, (d_{j+1} * prow + d_j) * row_bytes, from this
+// stream instead of forming it from the residue bytes (two 24-bit
+// multiplies and an add per column, ~3 % of the strip's issue time).  Same
+// layout as the row buffer: per residue block, [quad][lane][4 columns]
+// (4 KiB); the column after a group's last one takes the padding code.
+struct PairAddrArgs {
+    const uint4* res;          // residue blocks (compact or class codes)
+    uint4* out;                // [blocks * 256] uint4
+    const GroupDesc* groups;
+    uint32_t ngroups;
+    uint32_t prow;             // codes + 1 (the padding code is prow - 1)
+    uint32_t row_bytes;        // table row stride: (NP + 4) * 4, or (NPT + 4) * 4 without main strips
+};
+hipError_t launch_pair_addr(const PairAddrArgs& a, hipStream_t st);
 
 // pair_kernel's per-search pair tables, built on the device from the query
 // and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)

@@ -32,41 +32,10 @@
 #include <atomic>
 #include <type_traits>
 
-#include "kernels.h"
+#include "dp_common.h"
 
 namespace ssa {
 
-typedef short s2 __attribute__((ext_vector_type(2)));
-
-#define AS_U32(x) __builtin_bit_cast(uint32_t, (x))
-#define AS_S2(x) __builtin_bit_cast(s2, (uint32_t)(x))
-
-__device__ __forceinline__ s2 adds(s2 a, s2 b) { return __builtin_elementwise_add_sat(a, b); }
-__device__ __forceinline__ s2 vmax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ uint32_t perm(uint32_t hi_src, uint32_t lo_src, uint32_t sel) {
-    return __builtin_amdgcn_perm(hi_src, lo_src, sel);
-}
-__device__ __forceinline__ short sat16(int v) { return (short)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
-__device__ __forceinline__ uint32_t pack16(short lo, short hi) {
-    return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
-}
-
-// byte selectors for v_perm_b32(a, b, sel): bytes 0-3 of b, 4-7 of a
-constexpr uint32_t SEL_LO_BHI_HI_ALO = 0x05040302u;  // lo = b.hi,  hi = a.lo
-constexpr uint32_t SEL_LO_BLO_HI_ALO = 0x05040100u;  // lo = b.lo,  hi = a.lo
-constexpr uint32_t SEL_LO_BHI_HI_AHI = 0x07060302u;  // lo = b.hi,  hi = a.hi
-
-template <int NP>
-__device__ __forceinline__ void load_row(uint32_t (&dst)[NP], const uint32_t* row) {
-#pragma unroll
-    for (int i = 0; i < NP / 4; i++) {
-        const uint4 v = *(const uint4*)(row + 4 * i);
-        dst[4 * i + 0] = v.x;
-        dst[4 * i + 1] = v.y;
-        dst[4 * i + 2] = v.z;
-        dst[4 * i + 3] = v.w;
-    }
-}
 
 template <int NP, bool NW>
 __global__ void __launch_bounds__(64 * kWaves)
@@ -284,26 +253,6 @@ strip16_kernel(const StripArgs a) {
 // 0x7C00+ (inf/NaN), which v_pk_maximum3_f16 propagates into S; such lanes
 // go to wide_kernel.  Exact scores up to 0x7BFF - kF16Floor = 29695.
 // ---------------------------------------------------------------------------
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t fmax3(uint32_t a, uint32_t b, uint32_t c) {
-    const h2 m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_bit_cast(h2, a),
-                                                                            __builtin_bit_cast(h2, b)),
-                                               __builtin_bit_cast(h2, c));
-    return __builtin_bit_cast(uint32_t, m);
-}
-__device__ __forceinline__ uint32_t fmax2(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(h2, a),
-                                                                      __builtin_bit_cast(h2, b)));
-}
-__device__ __forceinline__ uint32_t psubsat16(uint32_t a, uint32_t b) {   // v_pk_sub_u16 clamp
-    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)));
-}
-__device__ __forceinline__ uint32_t padd16(uint32_t a, uint32_t b) {   // v_pk_add_u16 (wrapping)
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, a) + __builtin_bit_cast(u2, b));
-}
 
 template <int NP>
 __global__ void __launch_bounds__(64 * kWaves)
@@ -429,519 +378,6 @@ strip_f16m_kernel(const StripArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// SW and NW on f16 bit patterns with a PAIR-SYMBOL profile (the fast path).
-//
-// Values are 16-bit patterns v + base that order like the positive f16
-// numbers they encode (see strip_f16m_kernel): SW uses base = kF16Floor and
-// the local-alignment floor inside E's max3.  NW works on diagonal-relative
-// values X^(i,j) = X(i,j) - (i+j)R: the gap-extension adds
-// of E and F cancel (E^ <- max(E^, h^+Q), F^ <- max(F^, h^+Q)), the profile
-// carries -2R, all boundaries become constants, and the score is
-// H^(m-1,len-1) + (m+len-2)R.  Its base a.nw_base is chosen on the host so
-// that every real value and intermediate of entries up to a.nmax16 columns
-// stays inside [0x0400, 0x7BFF] -- NW needs no floor and no
-// saturation.  Padding rows/columns may leave that range;
-// nothing real depends on them (dependencies only run down and right, and a
-// borrow only runs from a low half into the high half, whose cell is at the
-// same or a later column and row).
-//
-// The packed profile operand of one column is (QP[d_j][r], QP[d_{j-1}][r+NP]):
-// low half for the current residue, high half for the previous one (the
-// skew).  Indexing the LDS table by the residue pair (d_j, d_{j-1}) returns
-// it directly -- no v_bfi_b32 per cell and no VGPR copy of the previous row.
-// The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB alphabet,
-// +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is shared by
-// the workgroup's waves, so they step through the strips together (one
-// barrier per strip; groups of a workgroup are adjacent in the length order,
-// so their strips take nearly the same time).
-//
-// One launch covers the whole query: a.nstrips strips of 2*NP rows from row
-// 0, then -- when NPT > 0 -- one final strip of 2*NPT rows with its own table
-// (a.qpt_tail).  The host (engine.cpp) picks NPT as the smallest multiple of 4
-// (8 rows) that holds the remainder, so a 400-row query runs 8 strips of 48
-// rows and one of 16 instead of a half-empty 48-row strip, and without a
-// second launch (a separate launch of the short strip cost its
-// own grid ramp and prologue: ~20 % above its instruction count).  NW always
-// runs its last strip as the tail: it captures H(m-1, len-1), a per-column
-// select that only the tail's instantiation carries (in the main strips'
-// code it raised the register allocation past the 3-waves limit).
-//
-// Columns are processed up to GroupDesc::ncols (a multiple of 4, >= the
-// group's longest entry + 1) in 16-column residue blocks with a uniform exit
-// inside the last block.
-// ---------------------------------------------------------------------------
-// row groups of the SW anti-diagonal maxima: 16, then 8, then 4 rows
-constexpr int ad_size_at(int s, int np) { return np - s >= 16 ? 16 : (np - s >= 8 ? 8 : 4); }
-constexpr int ad_start(int r, int np) {
-    int s = 0;
-    while (r >= s + ad_size_at(s, np)) s += ad_size_at(s, np);
-    return s;
-}
-constexpr int ad_size(int r, int np) { return ad_size_at(ad_start(r, np), np); }
-constexpr int ad_index(int r, int np) {
-    int s = 0, i = 0;
-    while (r >= s + ad_size_at(s, np)) s += ad_size_at(s, np), i++;
-    return i;
-}
-constexpr int ad_ngroups(int np) { return ad_index(np - 1, np) + 1; }
-
-// waves per workgroup (they share the pair table) and waves per SIMD the
-// register budget is sized for.  (64-row strips, NP = 32, were tried: their
-// 63.5 KiB table allows two workgroups per CU, and at 3-4 waves/SIMD the
-// strip's state no longer fits the registers -- they spill in the DP loop.)
-constexpr int pair_waves(int, bool) { return kPairWaves; }
-constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : (np <= 24 ? 3 : 2); }
-
-// where a wave runs, for the timeline: XCC << 16 | HW_ID[15:0] (wave slot,
-// SIMD, pipe, CU, shader array, SE)
-__device__ inline uint32_t hw_place() {
-    uint32_t id, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    return (xcc & 0xffu) << 16 | (id & 0xffffu);
-}
-
-// Strip parts (StripArgs::nparts = 2) hand a group's boundary rows from the
-// workgroup of part 0 (XCD A) to that of part 1 (maybe XCD B; the XCDs' L2s
-// are not coherent).  Part 0 keeps its strip boundaries in the row buffer as
-// usual, but writes its LAST boundary -- the one part 1 reads -- with
-// device-scope 16-byte stores (a buffer store with the sc1 bit: write-through
-// past A's L2, full lines), then waits for them (vmcnt 0) before the flag.
-// Part 1 reads that boundary with ordinary loads (B's L1/L2 never held these
-// lines in this kernel: dispatch invalidates them) and keeps its own
-// boundaries in a second row buffer (StripArgs::rowbuf2), so no dirty line
-// of the first buffer left in A's L2 can ever be written back over newer
-// data.  No cache-wide writeback/invalidate (those stalled every XCD: -3 %
-// on C2); the row-buffer traffic is unchanged.  Two parts at most.
-__device__ __forceinline__ void store_row(uint4* p, uint4 v, bool dev, __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
-    if (dev) {
-        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-        const v4u x = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, 0, 16 /* sc1 */);
-    } else {
-        *p = v;
-    }
-}
-
-template <int NP, bool NW, int NPT>
-__global__ void __launch_bounds__(64 * pair_waves(NP, NW), pair_occupancy(NP, NW))
-pair_kernel(const StripArgs a) {
-    constexpr int W = pair_waves(NP, NW);
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t wg = blockIdx.x;
-    if (a.ticket) {
-        // (through the table's first LDS dword: the first strip's staging
-        // starts behind a barrier, after every wave has read it; a static
-        // __shared__ word would not fit beside a 160 KiB table)
-        if (threadIdx.x == 0) lds[0] = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        wg = __builtin_amdgcn_readfirstlane(lds[0]);
-    }
-    // several queries (StripArgs::nq): unit = (part, quad, query), query innermost
-    const uint32_t nqs = a.nq > 1 ? a.nq : 1u;
-    uint32_t qi = 0;
-    if (nqs > 1) {
-        const uint32_t u = wg;
-        wg = u / nqs;
-        qi = u - wg * nqs;
-    }
-    // strip parts (StripArgs::nparts): unit wg = part `part` of quad wg
-    uint32_t part = 0;
-    if (a.nparts > 1) {
-        part = wg / a.nquads;
-        wg -= part * a.nquads;
-        if (part > 0) {
-            // the group's previous part must be done: its strip boundary rows
-            // (row buffer) and running maxima come from that workgroup.  Its
-            // unit had a lower ticket, so it is resident or finished: the wait
-            // ends (bounded anyway -- a timeout is reported, never a hang)
-            if (threadIdx.x == 0) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(a.part_done + (size_t)wg * nqs + qi, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) < part) {
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {       // 0.5 s
-                        __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(4);
-                }
-            }
-            __syncthreads();
-        }
-    }
-    const uint32_t g = a.g_first + wg * W + wave;
-    const bool active = g < a.ngroups;
-    if (g < a.g_prio) __builtin_amdgcn_s_setprio(2);
-    const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
-    const uint32_t gg = active ? g : a.g_first;
-
-    // this unit's query: rows, tables, outputs
-    const uint32_t m = nqs > 1 ? a.qm[qi] : a.m;
-    const uint32_t* const qpt = a.qpt + qi * a.q_tab_stride;
-    const uint32_t* const qpt_tail = a.qpt_tail + qi * a.q_tab_stride;
-    int32_t* const scores = a.scores + qi * a.q_score_stride;
-    uint32_t* const ovf_list = a.ovf_list + qi * a.q_ovf_stride;
-    uint32_t* const ovf_count = a.ovf_count + qi * a.q_ovf_stride;
-
-    const GroupDesc gd = a.groups[gg];
-    const uint32_t nquads = gd.ncols >> 2;
-    const uint32_t nblk = (gd.ncols + 15) >> 4;
-    const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
-    // row buffers: rb0 (part 0, and every strip without parts), rb1 (part
-    // 1's own boundaries); rbr / rbw: where the current strip reads its top
-    // boundary and writes its bottom one
-    uint4* const rb0 = a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane;
-    uint4* const rb1 = a.nparts > 1 ? a.rowbuf2 + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256 + lane : rb0;
-    uint4* rbr = rb0;
-    uint4* rbw = part > 0 ? rb1 : rb0;
-    // the handoff strip's device-scope stores (part 0's last strip)
-    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256), 0, 0x7fffffff, 0x00020000);
-    bool handoff = false;
-    const uint32_t gl = gg * 64 + lane;
-    const uint32_t prow = a.alpha + 1;
-    const uint32_t len = a.lane_len[gl];
-
-    constexpr uint32_t FL = (uint32_t)kF16Floor * 0x10001u;
-    const int Q = a.gap_open, R = a.gap_extend;
-    const int BASE = NW ? (int)a.nw_base : kF16Floor;
-    const uint32_t cQ = (uint32_t)(Q * 65536 + Q);      // "combined": one v_add_u32 updates both halves
-    auto pat = [&](int v) -> uint32_t { return (uint32_t)(v + BASE) & 0xffffu; };
-
-    // SW: running max of x = sat(h - floor(next column)) = max(H - |R|, 0),
-    // an exact H_max + (-|R|) unless it is 0 (then the lane is re-scored)
-    const uint32_t Rabs = (uint32_t)(-R);
-    const uint32_t cRabs = Rabs * 0x10001u;
-    uint32_t* const smax = a.part_smax + (size_t)qi * a.ngroups * 64;
-    uint32_t S = (!NW && part > 0 && active) ? __hip_atomic_load(smax + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                             : 0u;
-
-    // NW: H(m-1, len-1) as captured by the tail strip, and which half of it
-    uint32_t cap = 0;
-    int cap_half = 0;
-
-    // One strip of height 2*NPS from query row i0, table at src.  CAPS: the
-    // strip holding row m-1 of an NW search (captures its H).
-    auto strip = [&](auto np_c, auto cap_c, int i0, const uint32_t* tab) {
-        constexpr int NPS = decltype(np_c)::value;
-        constexpr bool CAPS = decltype(cap_c)::value;
-        constexpr int ROWW = NPS + 4;
-        // ---- the whole workgroup stages this strip's pair table
-        __syncthreads();
-        const uint32_t ntab4 = prow * prow * (NPS / 4);
-        const uint4* src = (const uint4*)tab;
-        for (uint32_t i = threadIdx.x; i < ntab4; i += 64 * W) {
-            const uint32_t row = i / (NPS / 4), k = i % (NPS / 4);
-            *(uint4*)(lds + row * ROWW + 4 * k) = src[i];
-        }
-        __syncthreads();
-        if (!active) return;
-        const bool first = (i0 == 0);
-        // the last strip's boundary row has no reader
-        const bool keep = i0 + 2 * NPS < (int)m;
-        const int rr = (int)m - 1 - i0;          // strip row of the last query row (CAPS)
-        if (CAPS) cap_half = rr >= NPS ? 1 : 0;
-        const int cap_row = rr - cap_half * NPS;
-        const uint32_t cap_col = len - 1 + cap_half;
-        // the wave's capture columns span [cmin, cmax] (lengths are sorted, so
-        // the span is narrow): the select runs only there, behind a scalar test
-        uint32_t cmin = 0, cmax = 0;
-        if (CAPS) {
-            uint32_t lo = len ? cap_col : 0xffffffffu, hi = len ? cap_col : 0u;
-            for (int o = 32; o > 0; o >>= 1) {
-                lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
-                hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
-            }
-            cmin = __builtin_amdgcn_readfirstlane(lo);
-            cmax = __builtin_amdgcn_readfirstlane(hi);
-        }
-
-        // ---- left boundary (column -1).  SW: 0.  NW, diagonal-relative
-        // (X^(i,j) = X(i,j) - (i+j)R): H^(i,-1) = Q+2R, E^ into column 0 =
-        // 2Q+2R, H^(-1,j) = Q+2R, F^ into row 0 = 2Q+2R, H^(-1,-1) = 2R --
-        // constants.  High halves: step 0 runs them over the virtual column
-        // -1, and the initial values make that step produce the boundary by
-        // itself: diagonal input Q+4R plus the padding profile -2R, E and F at
-        // the pattern minimum, so h = Q+2R and E leaves it as h+Q.
-        // SW, also diagonal-relative: true 0 is the pattern of (i+j)|R|, so
-        // the local-alignment floor differs per row and column: fl[r] holds
-        // the floor of the next column for both halves of row r (wave-
-        // uniform, SGPRs, +|R| per column).  Boundary H(i,-1) = 0 ->
-        // (i-1)|R|; high halves at step 0: E at the boundary value, the
-        // diagonal input and F low, so h = (i-1)|R|.
-        uint32_t H[NPS], E[NPS], fl[NPS];
-#pragma unroll
-        for (int r = 0; r < NPS; r++) {
-            if (NW) {
-                H[r] = pat(Q + 2 * R) | (pat(Q + 4 * R) << 16);
-                E[r] = pat(2 * Q + 2 * R) | (0x0400u << 16);
-            } else {
-                H[r] = pat((i0 + r - 1) * (int)Rabs) | (pat(0) << 16);
-                E[r] = pat((i0 + r) * (int)Rabs) | (pat((i0 + NPS + r - 1) * (int)Rabs) << 16);
-                fl[r] = __builtin_amdgcn_readfirstlane(pat((i0 + r + 1) * (int)Rabs) |
-                                                       (pat((i0 + NPS + r) * (int)Rabs) << 16));
-            }
-        }
-        // diagonal input of row i0 at column 0, H(i0-1, -1); high half low
-        uint32_t hd0 = NW ? pat(first ? 2 * R : Q + 2 * R) | (pat(Q + 4 * R) << 16)
-                          : pat((i0 - 2) * (int)Rabs) | (pat(0) << 16);
-        uint32_t Fprev = 0x0400u;
-        // the boundary row above the strip: the previous strip's row buffer,
-        // or for the first strip the lane-independent top boundary a.top
-        // (a broadcast read; no per-column select between the two)
-        const uint4* qsrc = first ? a.top : rbr;
-        const uint32_t qstride = first ? 1 : 64;
-
-        // SW, anti-diagonal maxima (AD): cells (r, j) and (r+1, j-1) have the
-        // same diagonal-relative offset i0+r+j, so the running maximum needs no
-        // per-cell floor subtraction when it is taken along anti-diagonals.
-        // The strip's rows are split into groups of 16/8/4 rows (ad_group);
-        // in a group of G rows from row g, A[g + (a - g) % G] collects
-        // anti-diagonal a: at column j every even local row adds its new h and
-        // the previous column's H of the row below (one max3 per two cells);
-        // the group's anti-diagonal g+j is complete after its first row at
-        // column j and is flushed into S with one saturating subtract of its
-        // floor (= that row's floor fl[g]).  G divides the 16-column block, so
-        // every register index is static.
-        constexpr bool AD = !NW;
-        // floors advance right after their row's last use (fewer live SGPRs;
-        // measured neutral at 16 rows, -0.7 % at 24, where they fit anyway)
-        constexpr bool FL_INROW = NPS <= 16;
-        constexpr int NG = ad_ngroups(NPS);
-        uint32_t A[AD ? NPS : 1];
-#pragma unroll
-        for (int p = 0; p < (AD ? NPS : 1); p++) A[p] = 0;
-        uint32_t xa[2] = {0, 0};
-
-        uint32_t ob[4] = {0, 0, 0, 0};
-        uint4 rnext = resp[0];
-        // row-buffer quads prefetched PF quads ahead (NW's shorter steps
-        // need the longer distance to cover HBM latency)
-        constexpr int PF = NW ? 2 : 1;
-        uint4 qn[PF];
-#pragma unroll
-        for (int p = 0; p < PF; p++)
-            qn[p] = (uint32_t)p >= nquads ? make_uint4(0, 0, 0, 0) : qsrc[(size_t)p * qstride];
-        // pair row (d_0, pad) for column 0; later rows (d_j, d_{j-1})
-        // LDS byte offsets: the pair row (d_j, d_{j-1}) sits at
-        // d_j * pairB + d_{j-1} * rowB; the previous residue's term is kept
-        // pre-scaled, so a column's address is one 24-bit multiply-add (the
-        // 32-bit form compiled to v_mad_u64_u32 + v_mul_lo_u32 + a base add)
-        constexpr uint32_t rowB = ROWW * 4;
-        const uint32_t pairB = prow * rowB;
-        const char* ldsb = (const char*)lds;
-        uint32_t dprevB = a.alpha * rowB;
-        // P: the current column's profile operands.  The next column's row
-        // is loaded into P in place behind the row loop, four rows at a time
-        // (no second buffer: the registers pay for the SW accumulators A)
-        uint32_t P[NPS];
-        {
-            const uint32_t d0 = rnext.x & 0xffu;
-            load_row<NPS>(P, (const uint32_t*)(ldsb + (__umul24(d0, pairB) + dprevB)));
-            dprevB = __umul24(d0, rowB);
-        }
-
-        for (uint32_t b = 0; b < nblk; b++) {
-            const uint4 rcur = rnext;
-            if (b + 1 < nblk) rnext = resp[(size_t)(b + 1) * 64];
-            const uint32_t rw[4] = {rcur.x, rcur.y, rcur.z, rcur.w};
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                if (b * 4 + t >= nquads) break;      // uniform: the group's last columns
-                const uint4 qcur = qn[0];
-#pragma unroll
-                for (int p = 0; p + 1 < PF; p++) qn[p] = qn[p + 1];
-                {
-                    const uint32_t nq = b * 4 + t + PF;
-                    if (nq < nquads) qn[PF - 1] = qsrc[(size_t)nq * qstride];
-                }
-                const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int k = t * 4 + u;
-                    const uint32_t j = b * 16 + k;
-                    const uint32_t* nrow;
-                    {
-                        const uint32_t dn = k < 15 ? (rw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu
-                                                   : (rnext.x & 0xffu);
-                        nrow = (const uint32_t*)(ldsb + (__umul24(dn, pairB) + dprevB));
-                        dprevB = __umul24(dn, rowB);
-                    }
-                    const uint32_t rbv = qw[u];
-                    uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
-                    uint32_t hd = hd0;
-                    uint32_t xs[2];
-#pragma unroll
-                    for (int r = 0; r < NPS; r++) {
-                        // the diagonal step: P holds combined signed constants
-                        // (pair_tables_kernel), so one full-rate v_add_u32
-                        // replaces the half-rate v_pk_add_u16 (-5 % per row,
-                        // profiles/r01/ubench_mix_rates.txt)
-                        const uint32_t h = fmax3(hd + P[r], E[r], F);
-                        if ((r & 3) == 3) {
-                            const uint4 v = *(const uint4*)(nrow + r - 3);
-                            P[r - 3] = v.x;
-                            P[r - 2] = v.y;
-                            P[r - 1] = v.z;
-                            P[r] = v.w;
-                        }
-                        hd = H[r];
-                        const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
-                        if (AD && ((r - g0) & 1) == 0) {
-                            // H[r + 1] still holds column j-1
-                            const int ai = g0 + (r - g0 + k) % G;
-                            A[ai] = (r - g0 == G - 2) ? fmax2(h, H[r + 1]) : fmax3(A[ai], h, H[r + 1]);
-                        }
-                        H[r] = h;
-                        if (NW) {
-                            // diagonal-relative: E and F need no extension add
-                            const uint32_t tt = h + cQ;
-                            E[r] = fmax2(E[r], tt);
-                            F = fmax2(F, tt);
-                        } else {
-                            const uint32_t tt = h + cQ;
-                            E[r] = fmax3(E[r], tt, fl[r]);
-                            F = fmax2(F, tt);
-                            if (!AD) {
-                                // x = max(H - |R|, 0) into H[r]'s slot of the S tree
-                                xs[r & 1] = psubsat16(h, fl[r]);
-                                if (r & 1) S = fmax3(S, xs[0], xs[1]);
-                            }
-                            if (AD && r == g0) {
-                                // the group's anti-diagonal g0+j is complete:
-                                // x = max(H - |R|, 0).  One group: S takes two
-                                // columns' x per max3; several: two groups'.
-                                const uint32_t x = psubsat16(A[g0 + k % G], fl[g0]);
-                                const int gi = ad_index(r, NPS);
-                                if (NG == 1) {
-                                    xa[k & 1] = x;
-                                    if (k & 1) S = fmax3(S, xa[0], xa[1]);
-                                } else if (gi & 1) {
-                                    S = fmax3(S, xa[0], x);
-                                } else if (gi == NG - 1) {
-                                    S = fmax2(S, x);
-                                } else {
-                                    xa[0] = x;
-                                }
-                            }
-                            // row r's floor for the next column, updated in
-                            // place right after its last use (SGPRs are tight)
-                            if (FL_INROW) fl[r] += cRabs;
-                        }
-                    }
-                    if (!NW && !FL_INROW) {
-#pragma unroll
-                        for (int r = 0; r < NPS; r++) fl[r] += cRabs;
-                    }
-                    hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
-                    Fprev = F;
-                    // a per-step anchor the scheduler cannot move work across
-                    // (without it NW's schedule grows past 128 VGPRs and spills)
-                    if (!NW) asm volatile("" : "+v"(S));
-                    else asm volatile("" : "+v"(Fprev));
-                    // step 0's high half is the virtual column -1: no output
-                    if (b != 0 || k != 0) {
-                        ob[(k + 3) & 3] = perm(F, H[NPS - 1], SEL_LO_BHI_HI_AHI);
-                        if ((k & 3) == 0 && keep)
-                            store_row(rbw + (size_t)(b * 4 + (k >> 2) - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]),
-                                      handoff, rs0, ((b * 4 + (k >> 2) - 1) * 64 + lane) * 16);
-                    }
-                    if (CAPS && j >= cmin && j <= cmax) {
-                        uint32_t hsel = H[0];
-#pragma unroll
-                        for (int r = 1; r < NPS; r++) hsel = (cap_row == r) ? H[r] : hsel;
-                        cap = (j == cap_col) ? hsel : cap;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-        ob[3] = FL;
-        if (keep)
-            store_row(rbw + (size_t)(nquads - 1) * 64, make_uint4(ob[0], ob[1], ob[2], ob[3]), handoff, rs0,
-                      ((nquads - 1) * 64 + lane) * 16);
-        // the next strip reads what this one wrote (part 1 after its first
-        // strip: its own buffer)
-        rbr = rbw;
-        if (AD) {
-            // drain after the last column J = ncols-1: the odd local rows'
-            // cells of column J, and each group's anti-diagonals J+1 ..
-            // J+G-1 (partial).  fl[] now hold column J+1's floors; register
-            // g+p holds the group's anti-diagonal J+1+d, d = (p - ncols) mod G,
-            // floor fl[g] + d|R| (d = G-1 is anti-diagonal J, already
-            // flushed: skipped).
-#pragma unroll
-            for (int r = 0; r < NPS; r++) {
-                const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
-                if ((r - g0) & 1) S = fmax2(S, psubsat16(H[r], fl[r] - cRabs));
-                const uint32_t d = ((uint32_t)(r - g0) - gd.ncols) & (G - 1);
-                const uint32_t f = d == (uint32_t)G - 1 ? 0xffffffffu : fl[g0] + d * cRabs;
-                S = fmax2(S, psubsat16(A[r], __builtin_amdgcn_readfirstlane(f)));
-            }
-        }
-    };
-
-    using MainNP = std::integral_constant<int, NP>;
-    using TailNP = std::integral_constant<int, NPT ? NPT : 8>;
-    // this unit's strips [s0, s1) of the nstrips main strips + the tail strip
-    const uint32_t T = a.nstrips + (NPT > 0 ? 1u : 0u);
-    const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
-    const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
-    for (uint32_t s = s0; s < min(s1, a.nstrips); s++) {
-        handoff = a.nparts > 1 && part == 0 && s + 1 == s1;
-        strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, qpt + (size_t)s * prow * prow * NP);
-    }
-    if (NPT > 0 && s1 == T) {
-        handoff = false;
-        strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, qpt_tail);
-    }
-
-    if (a.nparts > 1 && part + 1 < a.nparts) {
-        // hand the group on: running maxima, then (after every wave's row
-        // buffer stores and maxima are visible at agent scope) the part count
-        if (!NW && active) __hip_atomic_store(smax + gl, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // every wave's device-scope stores complete, then one flag store
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, part + 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (!active) return;
-    if (a.timeline && lane == 0)
-        a.timeline[g - a.g_first] = make_uint4(g, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
-    const uint32_t o = a.lane_out[gl];
-    if (o == 0xffffffffu) return;
-    if (len == 0) {
-        scores[o] = NW ? (int32_t)(a.gap_open + (int64_t)m * a.gap_extend) : 0;
-        return;
-    }
-    int32_t score;
-    bool ovf = len > a.nmax16;
-    if (!NW) {
-        const uint32_t slo = S & 0xffffu, shi = S >> 16;
-        const uint32_t smax = slo > shi ? slo : shi;
-        // 0 leaves H_max in [0, |R|] undecided: re-score exactly
-        ovf = ovf || (smax == 0 && Rabs != 0);
-        score = (int32_t)smax + (int32_t)Rabs;
-    } else {
-        // back from the diagonal-relative value: + (i + j) R at (m-1, len-1)
-        score = (int32_t)(cap_half ? cap >> 16 : cap & 0xffffu) - BASE + ((int32_t)m + (int32_t)len - 2) * R;
-    }
-    if (ovf) {
-        const uint32_t idx = atomicAdd(ovf_count, 1u);
-        if (idx < a.ovf_cap) ovf_list[idx] = gl;
-        scores[o] = INT32_MIN;
-    } else {
-        scores[o] = score;
-    }
-}
 
 // Exact int64 re-score of overflowed lanes: the reference's 64-bit
 // recurrences verbatim (one lane per sequence, H/E column in HBM scratch).
@@ -1254,18 +690,43 @@ hipError_t launch_recode(const RecodeArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// hipFuncSetAttribute (dynamic LDS above 64 KiB) once per kernel and device:
-// the per-device search threads of a multi-GPU search launch concurrently
-static hipError_t lds_attr_once(const void* fn, std::atomic<uint64_t>& done, int bytes) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    const uint64_t bit = 1ull << (dev & 63);
-    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
-    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
-    return e;
+// ------------------------------------------------------------ pair rows
+// One wave per group, one lane per sequence: each residue block's 16
+// columns become four quads of pair-row offsets (kernels.h PairAddrArgs).
+__global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
+    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (g >= a.ngroups) return;
+    const GroupDesc gd = a.groups[g];
+    const uint32_t nblk = (gd.ncols + 15) >> 4;
+    const uint32_t pad = a.prow - 1;
+    const uint32_t pairB = a.prow * a.row_bytes;
+    uint4 cur = nblk ? a.res[(size_t)gd.blk * 64 + lane] : make_uint4(0, 0, 0, 0);
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint4 nxt = b + 1 < nblk ? a.res[(size_t)(gd.blk + b + 1) * 64 + lane] : make_uint4(pad, 0, 0, 0);
+        const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
+        uint32_t o[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t d = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            const uint32_t dn = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu;
+            // past the group's last column: the padding code
+            const uint32_t dnx = b * 16 + k + 1 < gd.ncols ? dn : pad;
+            o[k] = dnx * pairB + d * a.row_bytes;
+        }
+        uint4* dst = a.out + (size_t)(gd.blk + b) * 256 + lane;
+#pragma unroll
+        for (int t = 0; t < 4; t++) dst[t * 64] = make_uint4(o[4 * t], o[4 * t + 1], o[4 * t + 2], o[4 * t + 3]);
+        cur = nxt;
+    }
 }
+
+hipError_t launch_pair_addr(const PairAddrArgs& a, hipStream_t st) {
+    if (a.ngroups == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_addr_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 
 // ------------------------------------------------------------ long entries
 // The longest DB entries, so that a handful of entries far longer than the
@@ -2022,42 +1483,16 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int NP, bool NW, int NPT>
-static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
-    static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)pair_kernel<NP, NW, NPT>, attr, (int)kPairLdsMax);
-    if (e != hipSuccess) return e;
-    constexpr int W = pair_waves(NP, NW);
-    const uint32_t quads = (a.ngroups - a.g_first + W - 1) / W;
-    if (a.nparts > 1 && a.nquads != quads) return hipErrorInvalidValue;
-    if (a.nq > (uint32_t)kMaxFuse) return hipErrorInvalidValue;
-    const uint32_t blocks = quads * std::max(a.nparts, 1u) * std::max(a.nq, 1u);
-    hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
-    return hipGetLastError();
-}
 
-template <int NP, bool NW, int NPT = 4>
-static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st) {
-    // npt in {0} + multiples of 4 up to NP
-    if constexpr (NPT == 4) {
-        if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st);
-    }
-    if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st);
-    if constexpr (NPT + 4 <= NP) return launch_pair_np<NP, NW, NPT + 4>(a, npt, lds_bytes, st);
-    return hipErrorInvalidValue;
-}
+// pair_sw.hip / pair_nw.hip
+hipError_t launch_pair_sw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st);
+hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st);
 
 hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st) {
     if (a.ngroups <= a.g_first || (a.nstrips == 0 && npt == 0)) return hipSuccess;
     // NW scores come from the tail strip's capture
     if (nw && npt == 0) return hipErrorInvalidValue;
-    if (np == 24) return nw ? launch_pair_np<24, true>(a, npt, lds_bytes, st) : launch_pair_np<24, false>(a, npt, lds_bytes, st);
-    if (np == 32) return nw ? launch_pair_np<32, true>(a, npt, lds_bytes, st) : launch_pair_np<32, false>(a, npt, lds_bytes, st);
-    if (np == 40) return nw ? launch_pair_np<40, true>(a, npt, lds_bytes, st) : launch_pair_np<40, false>(a, npt, lds_bytes, st);
-    if (np == 36 && !nw) return launch_pair_np<36, false>(a, npt, lds_bytes, st);
-    if (np == 16) return nw ? launch_pair_np<16, true>(a, npt, lds_bytes, st) : launch_pair_np<16, false>(a, npt, lds_bytes, st);
-    if (np == 8) return nw ? launch_pair_np<8, true>(a, npt, lds_bytes, st) : launch_pair_np<8, false>(a, npt, lds_bytes, st);
-    return hipErrorInvalidValue;
+    return nw ? launch_pair_nw(a, np, npt, lds_bytes, st) : launch_pair_sw(a, np, npt, lds_bytes, st);
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

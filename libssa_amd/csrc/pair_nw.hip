@@ -1,0 +1,19 @@
+// pair_nw.hip -- the NW instantiations of pair_kernel (pair_kernel.h): main
+// strips of 2*np rows, a tail strip of 2*npt rows (npt a multiple of 4 up to
+// np, or 0).
+#include "pair_kernel.h"
+
+namespace ssa {
+
+hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st) {
+    switch (np) {
+    case 24: return launch_pair_np<24, true>(a, npt, lds_bytes, st);
+    case 32: return launch_pair_np<32, true>(a, npt, lds_bytes, st);
+    case 40: return launch_pair_np<40, true>(a, npt, lds_bytes, st);
+    case 16: return launch_pair_np<16, true>(a, npt, lds_bytes, st);
+    case 8: return launch_pair_np<8, true>(a, npt, lds_bytes, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace ssa
