@@ -124,7 +124,7 @@ struct DeviceDB {
     // and the class map it was made with
     uint4* d_res_cls = nullptr;
     std::vector<uint8_t> cls_key;
-    // pair_kernel main strips' pair-row stream (StripArgs::paddr, as
+    // pair_kernel's pair-row stream (StripArgs::paddr, as
     // d_rowbuf) and what it was built from: residue copy (class map), code
     // count + 1, row width
     uint4* d_paddr = nullptr;

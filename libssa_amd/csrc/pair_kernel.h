@@ -91,7 +91,7 @@ typedef __attribute__((address_space(3))) const u32x4 lds_u4;
 __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint4 v, bool dev) {
     const u32x4 x = {v.x, v.y, v.z, v.w};
     if (dev) __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, soff, 16 /* sc1 */);
-    else __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, soff, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, soff, 2 /* nt */);
 }
 // The per-group streams (row buffers, pair rows, top boundary) are read and
 // written through buffer resources based at the group's first block: the
@@ -100,8 +100,12 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, uint32_t vo
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
+// (aux: cache policy; the row buffer is written once and read once, so its
+// loads and stores are non-temporal: C2 +1 %, profiles/r03/stream/nt_pf_variants.txt;
+// the pair-row stream is re-read by every strip and keeps the default)
+template <int AUX = 0>
 __device__ __forceinline__ uint4 load_quad(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX);
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
@@ -316,7 +320,7 @@ pair_kernel(const StripArgs a) {
 #pragma unroll
         for (int p = 0; p < PF; p++) {
             const uint32_t nq = min((uint32_t)p, nquads - 1);
-            qn[p] = load_quad(qsrc, qvoff, nq * qstride);
+            qn[p] = load_quad<2>(qsrc, qvoff, nq * qstride);
             an[p] = load_quad(pap, lane16, nq * 1024u);
         }
         // P: the current column's profile operands, first the pair row
@@ -349,7 +353,7 @@ pair_kernel(const StripArgs a) {
                     // count exactly the loads issued after it
                     const uint32_t nq = min(b * 4 + t + PF, nquads - 1);
                     const int nb = PF == 1 ? ((t + 1) & 1) : PF - 1;
-                    qn[nb] = load_quad(qsrc, qvoff, nq * qstride);
+                    qn[nb] = load_quad<2>(qsrc, qvoff, nq * qstride);
                     an[nb] = load_quad(pap, lane16, nq * 1024u);
                 }
                 const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};

@@ -1538,6 +1538,42 @@ def test_overflow_counters_nw_matrix_maximum(waves, tmp_path):
 
 
 @pytest.mark.gpu
+def test_pair_row_stream_follows_the_plan():
+    """The pair kernel's per-column pair-row offsets (pair_addr_kernel) are
+    cached per DB and rebuilt when the table they address changes: row width
+    (48-, 32- and 80-row strips, tail-only queries at their own width) and
+    the per-query class map (queries with X / U, O on a 28-symbol DB).
+    Queries alternate back and forth so every rebuild is followed by reuse;
+    every full score vector equals the oracle's, SW and NW."""
+    codes, off = syn.protein_db_range(6000, 9, alphabet="uniform28", lengths="uniform", lo=1, hi=500)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    qs = []
+    for m, seed in ((400, 1), (20, 2), (60, 3), (130, 4), (7, 5)):
+        qs.append(syn.protein_query(m, seed))
+    qx = syn.protein_query(300, 6)
+    qx[::13] = syn.AA_ORDER.index("X")
+    qu = syn.protein_query(45, 7)
+    qu[::5] = syn.AA_ORDER.index("U")
+    qu[2::7] = syn.AA_ORDER.index("O")
+    order = [qs[0], qs[1], qx, qs[2], qu, qs[0], qs[3], qs[4], qx, qs[1], qu, qs[3]]
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        n = len(off) - 1
+        keep = np.nonzero(np.diff(off.astype(np.int64)) > 0)[0]
+        for i, q in enumerate(order):
+            qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+            for algo in (S.SW, S.NW):
+                exp = po.scores(algo, q, codes, off, M, -11, -1)
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all(), (i, algo)
+                assert (sc == exp[keep]).all(), (i, algo, len(q), np.nonzero(sc != exp[keep])[0][:10])
+                assert S.stats()["kernel"].startswith("pair"), S.stats()["kernel"]
+            S.free_sequence(qq)
+        assert n == len(off) - 1
+
+
+@pytest.mark.gpu
 def test_short_sw_queries_take_32_row_strips():
     """Short SW queries whose rows fill 32-row strips better (q <= 32 and
     48 < q <= 64) run the pair kernel's 32-row strips at four waves per SIMD
