@@ -62,17 +62,19 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # profiles/r02/pmc_c2_s3 (48-row SW strips, the default, 24-bit LDS address),
 # profiles/r02/pmc_c3_np40 (80-row NW strips, the default) and
 # profiles/r03/pmc_c2 (round 3: strip parts, long16_kernel; 6.654e9 x 64 /
-# 1.406e11 = 3.03).  Keyed by
-# (kernel, pair strip rows): the instruction count per cell depends on the
-# strip height.
-VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 3.03,
-                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.66}
+# 1.406e11 = 3.03) and profiles/r03/final/pmc_c2 / pmc_c3 (round 3: the
+# pair-row stream; SW 6.444e9 x 64 / 1.406e11 = 2.93, NW 80-row 1.439e10 x
+# 64 / 3.516e11 = 2.62).  Keyed by (kernel, pair strip rows): the instruction
+# count per cell depends on the strip height.
+VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 2.93,
+                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.62}
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
 # profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
-# (tools/hotloop.py: per 48-row column SW 49 of 142.8, NW 49 of 128.8; the
-# 80-row NW column's share scaled by the census ratio at 48 rows)
-VALU_FAST_SHARE = {("pair_f16_sw", 48): 0.343, ("pair_f16_nw", 48): 0.380, ("pair_f16_nw", 80): 0.387}
+# (tools/hotloop.py: per 48-row column SW 48 of 140.8 with the tail strip,
+# NW 49 of 128.8 in round 2; the 80-row NW column's share scaled by the
+# census ratio at 48 rows)
+VALU_FAST_SHARE = {("pair_f16_sw", 48): 0.341, ("pair_f16_nw", 48): 0.380, ("pair_f16_nw", 80): 0.387}
 
 
 def parse():
