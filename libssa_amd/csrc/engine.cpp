@@ -725,7 +725,7 @@ static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
 }
 
 // strip parts of a pair-kernel launch of T strips (StripArgs::nparts; at
-// most two: kernels.hip store_row's coherence argument).  Auto: two parts for
+// most two: pair_kernel.h store_row's coherence argument).  Auto: two parts for
 // groups of at least 4 strips -- C2 (9 strips) +1.1 %, C3 (13) +1.1 %, the
 // reference's benchmark shape (11) +6-8 %, q = 200 (5) +1 %; q = 100 (3)
 // -2.3 % (profiles/r03/parts_sweep.txt)

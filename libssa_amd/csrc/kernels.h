@@ -1,4 +1,5 @@
-// kernels.h -- argument blocks of the HIP kernels (kernels.hip).
+// kernels.h -- argument blocks of the HIP kernels (kernels.hip, counters.hip,
+// pair_kernel.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,7 +64,7 @@ struct StripArgs {
     // then all second parts.  A part waits until its group's previous part
     // is done (part_done[quad]); the handoff boundary crosses workgroups,
     // maybe XCDs, through device-scope stores, and part 1 keeps its own
-    // boundaries in rowbuf2 (kernels.hip store_row: the coherence argument,
+    // boundaries in rowbuf2 (pair_kernel.h store_row: the coherence argument,
     // which limits nparts to 2); the SW running maximum travels in
     // part_smax (one dword per lane).  The launch's last units are then
     // the shortest groups' second parts -- a fraction of a whole group's work
