@@ -12,7 +12,7 @@ namespace ssa {
 // SW and NW on f16 bit patterns with a PAIR-SYMBOL profile (the fast path).
 //
 // Values are 16-bit patterns v + base that order like the positive f16
-// numbers they encode (see strip_f16m_kernel): SW uses base = kF16Floor and
+// numbers they encode (see kernels.hip strip_f16m_kernel): SW uses base = kF16Floor and
 // the local-alignment floor inside E's max3.  NW works on diagonal-relative
 // values X^(i,j) = X(i,j) - (i+j)R: the gap-extension adds
 // of E and F cancel (E^ <- max(E^, h^+Q), F^ <- max(F^, h^+Q)), the profile
