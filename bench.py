@@ -1,18 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: GCUPS of the SW int16 database search on MI355X (BASELINE.json).
 
-Workload (BASELINE.json configs[1]): Smith-Waterman, BLOSUM62, gaps -11/-1,
-one 400-residue query against a synthetic 1 M-sequence protein DB (lengths
-1+Gamma(2,175) clipped to [16,4096], BLOSUM62 background, planted homologs;
-libssa_amd/synthetic.py), top-k = 10.  A step is one search: at N=1 the
-public sw_align() call (DB already packed in HBM, as the reference times
+Headline workload (BASELINE.json configs[1]): Smith-Waterman, BLOSUM62, gaps
+-11/-1, one 400-residue query against a synthetic 1 M-sequence protein DB
+(lengths 1+Gamma(2,175) clipped to [16,4096], BLOSUM62 background, planted
+homologs; libssa_amd/synthetic.py), top-k = 10.  A step is one search: at N=1
+the public sw_align() call (DB already packed in HBM, as the reference times
 sw_align with the DB pre-loaded, benchmark/src/benchmark_util.c:27-48); at
-N>1 each rank searches its own 1 M-sequence shard of an N M-sequence DB
-(weak scaling: global IDs rank*1M + i), returns its exact top-k insertion
-log, the logs are gathered to rank 0 over RCCL and replayed there
-(ssa_amd_replay), giving the bit-exact global result.
+N>1 each rank searches its own ~1 M-sequence slice of an N M-sequence DB
+(weak scaling, cut by residues), returns its exact top-k insertion log, the
+logs are gathered to rank 0 over RCCL and replayed there (ssa_amd_replay),
+giving the bit-exact global result.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|ref] [--seqs S]
+The same JSON line carries a "north_star" record (BASELINE.json north_star):
+SW int16, the same query against the FIXED 10 M-sequence DB (the c4full
+fixture), cut into N residue-balanced ID slices -- the strong-scaling point
+the driver's `--gpus 1/2/4/8` runs produce, top-k checked against the
+reference's own search of that DB.  --no-north-star skips it.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|ref|sprot|north_star] [--seqs S]
 
 Launch: under torchrun (WORLD_SIZE set) every process is one rank.  Without
 it, `--gpus N` with N > 1 makes this process a launcher that never imports
@@ -23,16 +29,17 @@ reference fans out and joins its workers inside one call,
 src/util/thread_pool.c:76-86, src/algo/manager.c:141-145).  N larger than
 the visible GPU count is refused, except as a gloo rehearsal
 (SSA_DIST_BACKEND=gloo: several ranks share a GPU, the exchange goes over
-gloo).  --launch-selftest runs only the launch (ranks, env, rendezvous,
-failure propagation) without the library.
+gloo; the line then says "rehearsal" and n_gpus counts physical GPUs).
+--launch-selftest runs only the launch (ranks, env, rendezvous, failure
+propagation, the rank layout) without the library.
 
-Other BASELINE.json configurations (parity/extra measurements; the default
+Other BASELINE.json configurations (libssa_amd/workloads.py; the default
 line is C2): --config c3 = NW BLOSUM50 -10/-2, 1000-residue query, 1 M
 sequences per GPU; c4 = SW BLOSUM62 -11/-1 (API width 8) over 10 M sequences
 split across the ranks (strong scaling); c5 = SW DNA +5/-4, gaps -4/-2,
 10 k-nt query vs 50 M reads of 150 nt split across the ranks (strong); ref =
 the reference's published benchmark shape (P18080, 513 aa, BLOSUM50 -3/-1,
-548,208 synthetic sequences).
+548,208 synthetic sequences); sprot = the same in Swiss-Prot's form.
 --seqs overrides the per-GPU sequence count of any config.
 """
 import argparse
@@ -48,6 +55,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from libssa_amd import workloads as W  # noqa: E402
+
+CONFIGS = W.CONFIGS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -93,6 +103,10 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-north-star", action="store_true",
+                   help="skip the north_star record (SW int16, q = 400 vs the fixed 10 M-sequence DB, strong)")
+    p.add_argument("--north-star-steps", type=int, default=None, help="timed steps of the north_star record "
+                   "(default: --steps, at most 10)")
     p.add_argument("--long-tail", type=int, default=None,
                    help="replace N DB sequences by 5k-35k-residue ones (a UniProt-like length tail)")
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
@@ -114,53 +128,27 @@ def parse():
     p.add_argument("--selftest-fail-rank", type=int, default=-1,
                    help="--launch-selftest: this rank exits with status 3 before the rendezvous")
     args = p.parse_args()
-    cfg = CONFIGS[args.config]
-    for key in ("qlen", "algo", "matrix", "gap_open", "gap_extend"):
-        if getattr(args, key) is None:
-            setattr(args, key, cfg[key])
-    args.db = cfg["db"]
-    if args.alphabet is None:
-        args.alphabet = cfg.get("alphabet", "bg20")
-    if args.long_tail is None:
-        args.long_tail = cfg.get("long_tail", 0)
-    args.width = cfg["width"]
-    args.strong = cfg["total_seqs"] is not None
     return args
 
 
-# BASELINE.json configs; "total_seqs" set = strong scaling (split across ranks)
-CONFIGS = {
-    "c2": dict(algo="sw", matrix="blosum62", gap_open=-11, gap_extend=-1, qlen=400, db="protein",
-               seqs=1_000_000, total_seqs=None, width=16),
-    "c3": dict(algo="nw", matrix="blosum50", gap_open=-10, gap_extend=-2, qlen=1000, db="protein",
-               seqs=1_000_000, total_seqs=None, width=16),
-    "c4": dict(algo="sw", matrix="blosum62", gap_open=-11, gap_extend=-1, qlen=400, db="protein",
-               seqs=None, total_seqs=10_000_000, width=8),
-    "c5": dict(algo="sw", matrix="const5_-4", gap_open=-4, gap_extend=-2, qlen=10_000, db="dna",
-               seqs=None, total_seqs=50_000_000, width=16),
-    # the shape of the reference's own published benchmark (BASELINE.md §1:
-    # query P18080, 513 aa, BLOSUM50, gaps -3/-1, UniProtKB/Swiss-Prot
-    # 2015_03 = 548,208 sequences; benchmark/src/benchmark_threads.c:36-46),
-    # on a synthetic DB of that sequence count (no network for Swiss-Prot)
-    "ref": dict(algo="sw", matrix="blosum50", gap_open=-3, gap_extend=-1, qlen=513, db="protein",
-                seqs=548_208, total_seqs=None, width=16, query_file="tests/golden/data/P18080.fasta"),
-    # the same in Swiss-Prot's form: its 25-symbol alphabet (+X, B, Z, U, O,
-    # util_sequence.c:36-44) and a length tail of 300 entries of 5-35 k
-    # residues (UniProt holds entries up to ~35 k); tests/golden/fullsize.json
-    # "sprot" pins it to the reference's own search
-    "sprot": dict(algo="sw", matrix="blosum50", gap_open=-3, gap_extend=-1, qlen=513, db="protein",
-                  seqs=548_208, total_seqs=None, width=16, query_file="tests/golden/data/P18080.fasta",
-                  alphabet="sprot25", long_tail=300),
-}
-
-
-def read_query_file(path):
-    """First FASTA record as synthetic-alphabet codes (the product parses
-    the same text itself through init_sequence_fasta)."""
-    from libssa_amd import synthetic as syn
-    lines = open(os.path.join(ROOT, path)).read().split("\n")
-    seq = "".join(l.strip() for l in lines[1:] if not l.startswith(">")).upper()
-    return np.array([syn.AA_ORDER.index(c) for c in seq], dtype=np.uint8)
+def workload(args, name, overrides=True):
+    """The config `name` with the command line's overrides (headline) or
+    exactly as defined (north_star), as one namespace."""
+    cfg = dict(CONFIGS[name])
+    w = argparse.Namespace(config=name, cfg=cfg, db=cfg["db"], width=cfg["width"],
+                           strong=cfg["total_seqs"] is not None, lengths="gamma", seqs=None,
+                           alphabet=cfg.get("alphabet", "bg20"), long_tail=cfg.get("long_tail", 0))
+    for key in ("qlen", "algo", "matrix", "gap_open", "gap_extend"):
+        v = getattr(args, key) if overrides else None
+        setattr(w, key, cfg[key] if v is None else v)
+    w.k, w.cpu_seconds = args.k, args.cpu_seconds
+    if overrides:
+        w.seqs, w.lengths = args.seqs, args.lengths
+        if args.alphabet is not None:
+            w.alphabet = args.alphabet
+        if args.long_tail is not None:
+            w.long_tail = args.long_tail
+    return w
 
 
 def matrix_table(name):
@@ -302,7 +290,7 @@ def launch(args, argv):
             if line.startswith("{"):
                 lines.append(line)
             else:
-                print(line, flush=True)
+                print(line, file=sys.stderr, flush=True)
     th = threading.Thread(target=pump, daemon=True)
     th.start()
     failed = None
@@ -341,6 +329,10 @@ def launch(args, argv):
     return 0
 
 
+def rehearsal_label(world, n_gpus, backend):
+    return f"{world} ranks on {n_gpus} GPU(s), exchange over {backend}"
+
+
 def launch_selftest(args):
     """A rank of `bench.py --gpus N --launch-selftest`: checks the launch
     environment and meets the other ranks over gloo (no library, no GPU)."""
@@ -352,61 +344,280 @@ def launch_selftest(args):
     if rank == args.selftest_fail_rank:
         print(f"rank {rank}: failing on purpose (--selftest-fail-rank)", file=sys.stderr, flush=True)
         sys.exit(3)
+    # the rank layout main() would use, from the GPU count the launcher saw
+    # (SSA_BENCH_VISIBLE_GPUS; absent in a selftest launch: one GPU assumed)
+    ngpu = int(os.environ.get("SSA_BENCH_VISIBLE_GPUS", "1"))
+    backend = os.environ.get("SSA_DIST_BACKEND", "nccl")
+    layout = {}
+    try:
+        device, rpg, n_gpus = W.rank_layout(world, ngpu, local, backend)
+        layout = {"device": device, "ranks_per_gpu": rpg, "n_gpus": n_gpus}
+        if rpg > 1:
+            layout["rehearsal"] = rehearsal_label(world, n_gpus, backend)
+    except SystemExit as e:
+        layout = {"refused": str(e)}
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "local_rank": local, "pid": os.getpid(),
-                                 "launcher": os.environ.get("SSA_BENCH_LAUNCHER")})
+                                 "launcher": os.environ.get("SSA_BENCH_LAUNCHER"), "layout": layout})
     dist.barrier()
     if rank == 0:
         print(json.dumps({"launch_selftest": "ok", "world": world, "ranks": got}), flush=True)
     dist.destroy_process_group()
 
 
-def make_shard(args, cfg, rank, world):
-    """This rank's contiguous ID slice of the config's synthetic DB, from the
-    block-seeded generators (libssa_amd/synthetic.py: a slice is
-    byte-identical to the same IDs of the whole DB).  Weak configs (C2/C3/ref):
-    an N x seqs DB, ~1 M per rank; strong ones (C4/C5): the fixed 10 M / 50 M
-    DB, so every N searches the same DB.  At N > 1 the ranks' ranges are cut
-    so that their residue sums balance (ssa_amd_shard_bounds),
-    not by sequence count.  At N = 1 C2 and C3 are exactly
-    tests/golden/fullsize.json's c2/c3 DBs.
-    --seqs: the per-rank sequence count of a weak config's DB, or the per-rank
-    share of a strong config's fixed DB (then cut by count: the first share is
-    the c4/c5 fixtures' DB).
-    Returns (query, codes, offsets, first global ID, DB size, IDs the job searches)."""
-    import libssa_amd as S
+class Job:
+    """The rank's view of the job: process group, gather path, timing."""
+
+    def __init__(self, rank, world, dist, dev, backend):
+        self.rank, self.world, self.dist, self.dev, self.backend = rank, world, dist, dev, backend
+        self.native = False          # ssa_amd_gather_logs over RCCL
+        self.gather_note = None
+        self.rccl_ranks = None
+        self.gather_checked = None
+
+    def reduce(self, x, op):
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def sum(self, x):
+        return self.reduce(x, None if self.dist is None else self.dist.ReduceOp.SUM)
+
+    def max(self, x):
+        return self.reduce(x, None if self.dist is None else self.dist.ReduceOp.MAX)
+
+    def min(self, x):
+        return self.reduce(x, None if self.dist is None else self.dist.ReduceOp.MIN)
+
+    def sync(self):
+        if self.dist is not None:
+            import torch
+            self.dist.barrier()
+            torch.cuda.synchronize()
+
+
+def setup_native_gather(S, job):
+    """N > 1: the shards' insertion logs meet on rank 0 in the library's own
+    RCCL gather (ssa_amd_gather_logs); the RCCL unique id travels over the
+    torch process group once."""
+    import torch
+    dist, rank, world = job.dist, job.rank, job.world
+
+    def agree(ok):
+        # every rank takes the same path: MIN over the ranks' flags
+        return job.min(1.0 if ok else 0.0) == 1.0
+    # 1. local readiness (RCCL resolvable, device selectable) agreed on
+    #    before anyone enters the collective ncclCommInitRank, so no rank
+    #    waits there for a peer that gave up
+    ready = S.dist_available()
+    if not ready:
+        job.gather_note = f"rank {rank}: RCCL not available to the library"
+    if not agree(ready):
+        job.gather_note = job.gather_note or "RCCL not available on another rank"
+        return
+    uid = None
+    if rank == 0:
+        try:
+            uid = S.dist_unique_id()
+        except RuntimeError as e:
+            job.gather_note = str(e)
+    obj = [uid]
+    dist.broadcast_object_list(obj, src=0)
+    ok = False
+    if obj[0] is not None:
+        try:
+            S.dist_init(rank, world, obj[0])
+            ok = True
+        except RuntimeError as e:
+            job.gather_note = str(e)
+    if not agree(ok):
+        if ok:
+            S.dist_finalize()
+        job.gather_note = job.gather_note or "RCCL setup failed on another rank"
+        return
+    job.native = True
+    job.rccl_ranks = S.dist_ranks()
+
+
+def check_native_gather(S, job, qq, algo, k, width):
+    """Untimed: the RCCL gather must equal the torch.distributed gather of
+    the same logs -- this search's, and a synthetic rising log of 600 rows
+    per rank at k = 600 (longer than the 512-row slot: the exact-size
+    ncclGather round).  Every rank joins every collective.  On any
+    disagreement the timed steps use the torch gather."""
+    import torch
+    from libssa_amd.dist import global_topk
+    rank = job.rank
+    log = S.search(qq, algo, k, width, S.LOG)
+    long_log = [(1000 * (rank * 600 + i) + 7, 10 ** 6 * rank + i, 0, 0, 0) for i in range(600)]
+    same = True
+    for lg, kk in ((log, k), (long_log, 600)):
+        a = S.gather_logs(lg, kk)
+        b = global_topk(lg, kk, job.dist, rank, job.world, job.dev)
+        if rank == 0:
+            same = same and [tuple(map(int, x[:2])) for x in a] == [tuple(map(int, x[:2])) for x in b]
+    flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=job.dev)
+    job.dist.broadcast(flag, src=0)
+    job.gather_checked = bool(int(flag.item()))
+    if not job.gather_checked:
+        S.dist_finalize()
+        job.native = False
+        job.gather_note = "RCCL gather disagreed with the torch.distributed gather: timed the torch gather"
+
+
+def configure(S, w):
+    dna = w.db == "dna"
+    S.init_symbol_translation(S.NUCLEOTIDE if dna else S.AMINOACID, S.FORWARD_STRAND, 1, 1)
+    if w.matrix.startswith("const"):
+        a, b = w.matrix[5:].split("_")
+        S.init_constant_scores(int(a), int(b))
+    else:
+        S.init_score_matrix(S.MATRIX_BUILDIN, w.matrix)
+    S.init_gap_penalties(w.gap_open, w.gap_extend)
+
+
+def load_shard(S, w, job):
+    """Untimed: this rank's contiguous ID slice of the workload's block-seeded
+    DB (libssa_amd/workloads.py: the cut is the one the GPU tests search),
+    written as FASTA, read through the plugin (init_db) and packed into HBM
+    with its global ID offset.  Returns a namespace of the slice."""
     from libssa_amd import synthetic as syn
-    dna = args.db == "dna"
-    if dna:
-        q = syn.dna_query(args.qlen, 8)
-    else:
-        q = read_query_file(cfg["query_file"]) if cfg.get("query_file") else syn.protein_query(args.qlen, 7)
-    hi = 4096 if args.lengths == "gamma" else 1000
-    if cfg["total_seqs"] is None:
-        per = args.seqs if args.seqs is not None else cfg["seqs"]
-        total = job = per * world
-        balanced = world > 1
-    else:
-        total = cfg["total_seqs"]
-        per = args.seqs if args.seqs is not None else (total + world - 1) // world
-        job = min(total, per * world)
-        balanced = world > 1 and args.seqs is None
-    if balanced and not dna:
-        lens = syn.protein_lengths_range(total, 42, 0, job, query=q, lo=16, hi=hi, lengths=args.lengths)
-        b = S.shard_bounds(lens, world)
-        i0, i1 = b[rank], b[rank + 1]
-    else:
-        # equal-length reads (C5), or one GPU: cutting by count is balanced
-        i0 = min(job, rank * per)
-        i1 = min(job, i0 + per) if rank + 1 < world else job
-    if dna:
-        codes, off = syn.dna_reads_range(total, 43, i0, i1, 150, query=q)
-        return q, codes, off, i0, total, job
-    codes, off = syn.protein_db_range(total, 42, i0, i1, query=q, alphabet=args.alphabet, lengths=args.lengths,
-                                      lo=16, hi=hi)
-    return q, codes, off, i0, total, job
+    configure(S, w)
+    t0 = time.time()
+    q = W.query(w.cfg, w.qlen)
+    bounds, total, job_ids = W.cuts(w.cfg, job.world, q, w.seqs, w.lengths)
+    i0, i1 = bounds[job.rank], bounds[job.rank + 1]
+    codes, off = W.slice_db(w.cfg, q, total, i0, i1, w.alphabet, w.lengths)
+    if w.db != "dna" and w.long_tail > 0:
+        # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
+        # residues of the DB's alphabet); the others keep theirs
+        codes, off = syn.with_long_tail(codes, off, w.long_tail, 77 + job.rank, w.alphabet)
+    tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{job.rank}_")
+    path = os.path.join(tmpdir, "db.fas")
+    syn.write_fasta(path, codes, off, nucleotide=w.db == "dna")
+    gen_s = time.time() - t0
+    t1 = time.time()
+    S.init_db(path)
+    S.set_id_offset(i0)
+    S.prepare_db()
+    os.remove(path)
+    os.rmdir(tmpdir)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=w.db == "dna"))
+    load_s = time.time() - t1
+    cells_local = float(off[-1]) * len(q)
+    return argparse.Namespace(q=q, qq=qq, codes=codes, off=off, id0=i0, total=total, job_ids=job_ids,
+                              seqs=len(off) - 1, residues=int(off[-1]), qlen=len(q), cells_local=cells_local,
+                              total_cells=job.sum(cells_local), gen_s=gen_s, load_s=load_s,
+                              setup_s=time.time() - t0)
+
+
+def timed_steps(S, job, sh, w, steps, warmup, k):
+    """W untimed warm-up steps, then exactly K steps between barrier +
+    synchronize on both sides; the max over ranks of the elapsed time."""
+    algo = S.SW if w.algo == "sw" else S.NW
+
+    def step():
+        if job.world == 1:
+            # the public sw_align / nw_align + free_alignment (libssa.h)
+            return S.align_scores(sh.qq, k, w.width, algo)
+        log = S.search(sh.qq, algo, k, w.width, S.LOG)
+        if job.native:
+            return S.gather_logs(log, k)
+        from libssa_amd.dist import global_topk
+        return global_topk(log, k, job.dist, job.rank, job.world, job.dev)
+
+    for _ in range(warmup):
+        step()
+    if job.native and job.gather_checked is None:
+        check_native_gather(S, job, sh.qq, algo, k, w.width)
+    job.sync()
+    per = {f: [] for f in ("kernel_ms", "wide_ms", "search_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms",
+                           "replay_ms")}
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        res = step()
+        st = S.stats()
+        for f in per:
+            per[f].append(st[f])
+    job.sync()
+    elapsed = job.max(time.perf_counter() - t_start)
+    return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=S.stats(),
+                              avg={f: float(np.mean(v)) for f, v in per.items()})
+
+
+def fixture_match(w, sh, res, k, world):
+    """The step's top-k against the reference's own search of this exact DB
+    (tests/golden/fullsize.json: c2, c3, the c4 / c5 shares, c4full = the
+    whole 10 M DB, c5full / c5share8, c2x2/4/8 = C2's weak-scaling DBs); at
+    N > 1 rank 0 holds the gathered global top-k of the N shards.  None when
+    no fixture is this DB."""
+    fxs = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))
+
+    def same_db(fx):
+        return (fx.get("kind", "protein") == w.db and w.alphabet == fx.get("alphabet", "bg20")
+                and w.lengths == fx.get("lengths", "gamma") and fx["n"] == sh.total and fx["i1"] == sh.job_ids
+                and w.long_tail == fx.get("tail", 0) and fx.get("query_file") == w.cfg.get("query_file")
+                and fx["qlen"] == sh.qlen and fx["algo"] == w.algo and fx["gap_open"] == w.gap_open
+                and fx["gap_extend"] == w.gap_extend and fx["matrix"] == w.matrix)
+    fx = next((f for f in fxs.values() if same_db(f)), None)
+    if res is None:
+        return None      # ranks > 0 hold no gathered result
+    if fx and (w.long_tail == 0 or world == 1) and k in (1, 10, 64):
+        return "match" if [list(map(int, x[:2])) for x in res] == fx[f"top{k}"] else "MISMATCH"
+    return None
+
+
+def traffic_key(w, sh, st):
+    """profiles/traffic.json key: the exact workload the PMC pass profiled."""
+    return (f"{w.config}:{w.algo}:{w.matrix}:{w.alphabet}:{w.lengths}:tail{w.long_tail}:seqs{sh.seqs}:"
+            f"q{sh.qlen}:rows{st['strip_rows']}")
+
+
+def north_star(S, args, job):
+    """BASELINE.json north_star as its own record: SW int16, BLOSUM62
+    -11/-1, the 400-residue query (seed 7) against the FIXED 10 M-sequence
+    DB of tests/golden/fullsize.json "c4full", cut into `world`
+    residue-balanced ID slices -- strong scaling, like the reference's own
+    thread-scaling benchmark (benchmark/src/benchmark_threads.c:34-60, timed
+    as benchmark/src/benchmark_util.c:27-48).  Each rank generates and packs
+    only its slice; the slices' logs meet through the same gather as the
+    headline; the top-k is checked against c4full's (the 64-bit replay,
+    width-independent)."""
+    w = workload(args, "north_star", overrides=False)
+    sh = load_shard(S, w, job)
+    steps = args.north_star_steps if args.north_star_steps is not None else min(args.steps, 10)
+    t = timed_steps(S, job, sh, w, steps, 1, args.k)
+    kms = t.avg["kernel_ms"]
+    kernel_gcups = sh.cells_local / (kms * 1e-3) / 1e9
+    value = sh.total_cells / (t.elapsed / steps) / 1e9
+    rec = {
+        "workload": "SW int16 BLOSUM62 gaps -11/-1, 400-residue query (seed 7) vs the fixed 10 M-sequence "
+                    "synthetic protein DB (tests/golden/fullsize.json c4full), residue-balanced ID slices per GPU",
+        "scaling": "strong", "bit_width": 16, "n_gpus": args.n_gpus, "ranks": job.world, "steps": steps, "warmup": 1,
+        "ms_per_step": round(t.elapsed / steps * 1e3, 3), "value": round(value, 2), "unit": "GCUPS",
+        "target_gcups": 1000.0, "meets_target": value >= 1000.0,
+        "db_total_seqs": sh.total, "db_total_residues": int(job.sum(sh.residues)),
+        "cells_per_step": sh.total_cells,
+        "rank0": {"seqs": sh.seqs, "residues": sh.residues, "kernel_ms": round(kms, 4),
+                  "kernel_gcups": round(kernel_gcups, 2)},
+        "kernel_ms_max_over_ranks": round(job.max(kms), 4),
+        "kernel_gcups_min_over_ranks": round(job.min(kernel_gcups), 2),
+        "hbm": {"algorithmic_bytes_rank0": float(t.st["kernel_bytes"]),
+                "frac_of_peak": float(t.st["kernel_bytes"]) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "setup_s": round(job.max(sh.setup_s), 1),
+        "top_hit": list(map(int, t.res[0][:2])) if t.res else None,   # (rank 0: the gathered result)
+        "gather": ("ssa_amd_gather_logs (RCCL)" if job.native else "torch.distributed") if job.world > 1 else None,
+    }
+    m = fixture_match(w, sh, t.res, args.k, job.world)
+    if m is not None:
+        rec["topk_vs_reference"] = m
+    S.free_sequence(sh.qq)
+    return rec
 
 
 def main():
@@ -424,22 +635,18 @@ def main():
     dist = None
     backend = os.environ.get("SSA_DIST_BACKEND", "nccl")   # nccl == RCCL on ROCm; gloo for rehearsal
     dev = "cuda" if backend == "nccl" else "cpu"
-    ranks_per_gpu = 1
+    ranks_per_gpu, args.n_gpus = 1, 1
     if world > 1:
         import torch
         import torch.distributed as dist
-        ngpu = torch.cuda.device_count()
-        if local >= ngpu:
-            if backend != "gloo":
-                raise SystemExit(f"bench.py rank {rank}: LOCAL_RANK {local} but only {ngpu} GPU(s) visible")
-            # gloo rehearsal: several ranks share a GPU
-            ranks_per_gpu = -(-world // max(1, ngpu))
-            local = local % max(1, ngpu)
+        # every rank derives the same layout from the world size and the
+        # visible GPU count (a gloo rehearsal shares GPUs between ranks)
+        local, ranks_per_gpu, args.n_gpus = W.rank_layout(world, torch.cuda.device_count(), local, backend)
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
+    job = Job(rank, world, dist, dev, backend)
 
     import libssa_amd as S
-    from libssa_amd import synthetic as syn
 
     S.load()
     S.set_device(local)
@@ -449,183 +656,56 @@ def main():
     for o in args.option:
         k, v = o.split("=")
         S.set_option(k, int(v))
-    dna = args.db == "dna"
-    S.init_symbol_translation(S.NUCLEOTIDE if dna else S.AMINOACID, S.FORWARD_STRAND, 1, 1)
-    if args.matrix.startswith("const"):
-        a, b = args.matrix[5:].split("_")
-        S.init_constant_scores(int(a), int(b))
-    else:
-        S.init_score_matrix(S.MATRIX_BUILDIN, args.matrix)
-    S.init_gap_penalties(args.gap_open, args.gap_extend)
-    algo = S.SW if args.algo == "sw" else S.NW
-    cfg = CONFIGS[args.config]
+    if world > 1 and backend == "nccl" and not args.torch_gather:
+        setup_native_gather(S, job)
 
-    # --- synthetic shard (untimed): generate, write FASTA, pack into HBM
-    t0 = time.time()
-    q, codes, off, id0, db_total, job_ids = make_shard(args, cfg, rank, world)
-    args.qlen = len(q)
-    args.seqs = len(off) - 1
-    if not dna and args.long_tail > 0:
-        # every (seqs / N)-th sequence becomes 5k-35k residues long (fresh
-        # residues of the DB's alphabet); the others keep theirs
-        codes, off = syn.with_long_tail(codes, off, args.long_tail, 77 + rank, args.alphabet)
-    tmpdir = tempfile.mkdtemp(prefix=f"ssa_bench_{rank}_")
-    path = os.path.join(tmpdir, "db.fas")
-    syn.write_fasta(path, codes, off, nucleotide=dna)
-    gen_s = time.time() - t0
-    t1 = time.time()
-    S.init_db(path)
-    S.set_id_offset(id0)
-    S.prepare_db()
-    os.remove(path)
-    os.rmdir(tmpdir)
-    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
-    load_s = time.time() - t1
-    setup_s = time.time() - t0
-    cells_local = float(off[-1]) * args.qlen
-    total_cells = cells_local
-    if dist is not None:
-        # the shards are cut by residues: sum the ranks' cells
-        import torch
-        tc = torch.tensor([cells_local], dtype=torch.float64, device=dev)
-        dist.all_reduce(tc, op=dist.ReduceOp.SUM)
-        total_cells = float(tc.item())
-
-    # N > 1: the shards' insertion logs meet on rank 0 in the library's own
-    # RCCL gather (ssa_amd_gather_logs); the RCCL unique id travels over the
-    # torch process group once
-    native = world > 1 and backend == "nccl" and not args.torch_gather
-    gather_note = None
-    rccl_ranks = None
-    if native:
-        import torch
-
-        def agree(ok):
-            # every rank takes the same path: MIN over the ranks' flags
-            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            return int(flag.item()) == 1
-        # 1. local readiness (RCCL resolvable, device selectable) agreed on
-        #    before anyone enters the collective ncclCommInitRank, so no rank
-        #    waits there for a peer that gave up
-        ready = S.dist_available()
-        if not ready:
-            gather_note = f"rank {rank}: RCCL not available to the library"
-        if agree(ready):
-            uid = None
-            if rank == 0:
-                try:
-                    uid = S.dist_unique_id()
-                except RuntimeError as e:
-                    gather_note = str(e)
-            obj = [uid]
-            dist.broadcast_object_list(obj, src=0)
-            ok = False
-            if obj[0] is not None:
-                try:
-                    S.dist_init(rank, world, obj[0])
-                    ok = True
-                except RuntimeError as e:
-                    gather_note = str(e)
-            if not agree(ok):
-                if ok:
-                    S.dist_finalize()
-                native = False
-                gather_note = gather_note or "RCCL setup failed on another rank"
-            else:
-                rccl_ranks = S.dist_ranks()
-        else:
-            native = False
-            gather_note = gather_note or "RCCL not available on another rank"
-
-    def step():
-        if world == 1:
-            # the public sw_align / nw_align + free_alignment (libssa.h)
-            return S.align_scores(qq, args.k, args.width, algo)
-        log = S.search(qq, algo, args.k, args.width, S.LOG)
-        if native:
-            return S.gather_logs(log, args.k)
-        from libssa_amd.dist import global_topk
-        return global_topk(log, args.k, dist, rank, world, dev)
-
-    def sync():
-        if dist is not None:
-            import torch
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    gather_checked = None
-    if native:
-        # untimed: the RCCL gather must equal the torch.distributed gather of
-        # the same logs -- this search's, and a synthetic rising log of 600
-        # rows per rank at k = 600 (longer than the 512-row slot: the
-        # exact-size ncclGather round).  Every rank joins every collective.
-        # On any disagreement the timed steps use the torch gather.
-        from libssa_amd.dist import global_topk
-        log = S.search(qq, algo, args.k, args.width, S.LOG)
-        long_log = [(1000 * (rank * 600 + i) + 7, 10 ** 6 * rank + i, 0, 0, 0) for i in range(600)]
-        same = True
-        for lg, kk in ((log, args.k), (long_log, 600)):
-            a = S.gather_logs(lg, kk)
-            b = global_topk(lg, kk, dist, rank, world, dev)
-            if rank == 0:
-                same = same and [tuple(map(int, x[:2])) for x in a] == [tuple(map(int, x[:2])) for x in b]
-        import torch
-        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=dev)
-        dist.broadcast(flag, src=0)
-        gather_checked = bool(int(flag.item()))
-        if not gather_checked:
-            S.dist_finalize()
-            native = False
-            gather_note = "RCCL gather disagreed with the torch.distributed gather: timed the torch gather"
-    sync()
-    kernel_ms, wide_ms, search_ms, d2h_ms, replay_ms, prep_ms, upload_ms, sync_ms = [], [], [], [], [], [], [], []
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-        st = S.stats()
-        kernel_ms.append(st["kernel_ms"])
-        wide_ms.append(st["wide_ms"])
-        search_ms.append(st["search_ms"])
-        prep_ms.append(st["prep_ms"])
-        upload_ms.append(st["upload_ms"])
-        sync_ms.append(st["sync_wait_ms"])
-        d2h_ms.append(st["d2h_ms"])
-        replay_ms.append(st["replay_ms"])
-    sync()
-    elapsed = time.perf_counter() - t_start
+    # --- the headline workload (BASELINE.json metric; default C2)
+    w = workload(args, args.config)
+    sh = load_shard(S, w, job)
+    t = timed_steps(S, job, sh, w, args.steps, args.warmup, args.k)
+    res, st = t.res, t.st
     if args.timeline and world == 1:
         # untimed: every DP wave's start/end on the s_memrealtime clock
         S.set_option("timeline", 1)
-        step()
+        t.step()
         np.save(args.timeline, S.timeline())
         S.set_option("timeline", 0)
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    st = S.stats()
-    if native:
+    S.free_sequence(sh.qq)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(sh.codes, sh.off, sh.q, matrix_table(w.matrix), w)
+        except Exception as e:  # report, never hide
+            cpu = {"value": None, "error": repr(e)}
+    match = fixture_match(w, sh, res, args.k, world)
+    codes_off = (sh.codes, sh.off)
+    sh.codes = sh.off = None
+    del codes_off
+
+    # --- the north-star record (strong scaling of the fixed 10 M DB)
+    ns = None if args.no_north_star else north_star(S, args, job)
+    if job.native:
         S.dist_finalize()
     if rank != 0:
         dist.destroy_process_group()
         return
-    ms_per_step = elapsed / args.steps * 1e3
-    gcups = total_cells / (elapsed / args.steps) / 1e9
-    kavg = float(np.mean(kernel_ms))
+
+    steps = args.steps
+    ms_per_step = t.elapsed / steps * 1e3
+    gcups = sh.total_cells / (t.elapsed / steps) / 1e9
+    kavg = t.avg["kernel_ms"]
+    cells_local = sh.cells_local
     # algorithmic bytes per launch: every residue once (1 B) + 4 B score per
     # sequence + the strip profile table
     alg_bytes = float(st["kernel_bytes"])
     achieved = alg_bytes / (kavg * 1e-3) / 1e9
-    traffic = None
+    tkey = traffic_key(w, sh, st)
+    traffic, tsrc = None, None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
-        rec = json.load(open(tf)).get(f"{args.algo}_{args.seqs}_{args.qlen}_pair{st['strip_rows'] // 2}")
+        rec = json.load(open(tf)).get(tkey)
         if rec:
-            traffic = rec["bytes_per_launch"]
+            traffic, tsrc = rec["bytes_per_launch"], rec["source"]
     # VALU issue roofline: VOP3/VOP3P instructions issue at
     # 4.17 cycles per wave64 instruction per SIMD, v_add_u32 at 2.5 (measured
     # in isolation: profiles/r01/ubench_valu_rates4.txt); instructions per
@@ -639,23 +719,25 @@ def main():
         "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
         "value": round(gcups, 2),
         "unit": "GCUPS",
-        "n_gpus": world,
+        "n_gpus": args.n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "strong" if w.strong else "weak",
         "vs_baseline": None,
         "dtype": "i16",
         "data": "synthetic",
-        "config": {"workload": f"{args.config.upper()}: {args.algo.upper()} {args.matrix} gaps {args.gap_open}/{args.gap_extend}, "
-                               f"{args.qlen}-residue query vs {args.seqs} synthetic {args.db} seqs per GPU "
-                               f"(mean len {float(off[-1]) / args.seqs:.1f}), top-{args.k}",
-                   "db_seqs_per_gpu": args.seqs, "db_total_seqs": db_total, "query_len": args.qlen, "residues_per_gpu": int(off[-1]),
-                   "cells_per_step": total_cells, "parallelism": f"db-shard x{world}", "job_seqs": job_ids, "pair_strip_rows": st["strip_rows"], "strip_np": args.strip_np,
-                   "bit_width": args.width},
+        "config": {"workload": f"{w.config.upper()}: {w.algo.upper()} {w.matrix} gaps {w.gap_open}/{w.gap_extend}, "
+                               f"{sh.qlen}-residue query vs {sh.seqs} synthetic {w.db} seqs per GPU "
+                               f"(mean len {sh.residues / max(sh.seqs, 1):.1f}), top-{args.k}",
+                   "db_seqs_per_gpu": sh.seqs, "db_total_seqs": sh.total, "query_len": sh.qlen,
+                   "residues_per_gpu": sh.residues, "cells_per_step": sh.total_cells,
+                   "parallelism": f"db-shard x{world}", "job_seqs": sh.job_ids, "pair_strip_rows": st["strip_rows"],
+                   "strip_np": args.strip_np, "bit_width": w.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey,
+                     "traffic_source": tsrc,
                      # the resource that actually binds this integer DP
                      "binding": {"bound": "valu_issue",
                                  "achieved": round(cells_local / (kavg * 1e-3) / 1e9, 2),
@@ -663,50 +745,33 @@ def main():
                                  "frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None}},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),
-                   "wide_ms_avg": round(float(np.mean(wide_ms)), 4), "wide_count": int(st["wide_count"]),
+                   "wide_ms_avg": round(t.avg["wide_ms"], 4), "wide_count": int(st["wide_count"]),
                    "valu_issue_bound_gcups": round(valu_bound / 1e9, 1) if valu_bound else None,
                    "valu_issue_frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None,
                    "valu_instr_per_cell": instr_per_cell},
-        "host_ms": {"search_call": round(float(np.mean(search_ms)), 3), "prep": round(float(np.mean(prep_ms)), 3),
-                    "upload": round(float(np.mean(upload_ms)), 3), "sync_wait": round(float(np.mean(sync_ms)), 3), "d2h_filter": round(float(np.mean(d2h_ms)), 3),
-                    "replay": round(float(np.mean(replay_ms)), 3)},
-        "setup_s": round(setup_s, 1),
-        "setup": {"generate_and_write_fasta_s": round(gen_s, 1), "init_db_and_pack_s": round(load_s, 1),
+        "host_ms": {"search_call": round(t.avg["search_ms"], 3), "prep": round(t.avg["prep_ms"], 3),
+                    "upload": round(t.avg["upload_ms"], 3), "sync_wait": round(t.avg["sync_wait_ms"], 3),
+                    "d2h_filter": round(t.avg["d2h_ms"], 3), "replay": round(t.avg["replay_ms"], 3)},
+        "setup_s": round(sh.setup_s, 1),
+        "setup": {"generate_and_write_fasta_s": round(sh.gen_s, 1), "init_db_and_pack_s": round(sh.load_s, 1),
                   "pack_ms": round(st["pack_ms"], 1)},
-        "top_hit": list(res[0]) if res else None,
-        "gather": ("ssa_amd_gather_logs (RCCL)" if native else "torch.distributed") if world > 1 else None,
-        "gather_equals_torch_gather": gather_checked,
-        "rccl_ranks": rccl_ranks,
+        "top_hit": list(map(int, res[0][:2])) if res else None,
+        "gather": ("ssa_amd_gather_logs (RCCL)" if job.native else "torch.distributed") if world > 1 else None,
+        "gather_equals_torch_gather": job.gather_checked,
+        "rccl_ranks": job.rccl_ranks,
         "launcher": os.environ.get("SSA_BENCH_LAUNCHER", "torchrun" if world > 1 else None),
     }
     if ranks_per_gpu > 1:
-        out["rehearsal"] = f"{world} ranks on {max(1, world // ranks_per_gpu)} GPU(s), exchange over {backend}"
-    if gather_note:
-        out["gather_note"] = gather_note
-    # the same DB and query as a reference-pinned fixture: the step's top-k
-    # against the reference's own (tests/golden/fullsize.json)
-    fxs = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))
-
-    def same_db(fx):
-        return (fx.get("kind", "protein") == args.db and args.alphabet == fx.get("alphabet", "bg20")
-                and args.lengths == fx.get("lengths", "gamma") and fx["n"] == db_total and fx["i1"] == job_ids
-                and args.long_tail == fx.get("tail", 0) and fx.get("query_file") == cfg.get("query_file")
-                and fx["qlen"] == args.qlen and fx["algo"] == args.algo and fx["gap_open"] == args.gap_open
-                and fx["gap_extend"] == args.gap_extend and fx["matrix"] == args.matrix)
-    # the fixture of this exact DB and search, if any (c2, c3, the c4 / c5
-    # shares, c4full = the whole 10 M DB, c5share8 = one GPU's C5 share at
-    # N = 8, c2x2/4/8 = C2's weak-scaling DBs): at N > 1 rank 0 holds the
-    # gathered global top-k of the N shards
-    fx = next((f for f in fxs.values() if same_db(f)), None)
-    if fx and (args.long_tail == 0 or world == 1) and args.k in (1, 10, 64):
-        out["topk_vs_reference"] = "match" if [list(x) for x in res] == fx[f"top{args.k}"] else "MISMATCH"
-    if world == 1 and not args.no_cpu_baseline:
-        from oracle import pyoracle as po
-        M = matrix_table(args.matrix)
-        try:
-            out["cpu_baseline"] = cpu_baseline(codes, off, q, M, args)
-        except Exception as e:  # report, never hide
-            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        out["ranks"] = world
+        out["rehearsal"] = rehearsal_label(world, args.n_gpus, backend)
+    if job.gather_note:
+        out["gather_note"] = job.gather_note
+    if match is not None:
+        out["topk_vs_reference"] = match
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    if ns is not None:
+        out["north_star"] = ns
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

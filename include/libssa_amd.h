@@ -61,6 +61,8 @@ typedef struct {
     uint32_t long_entries;   /* lanes (64 per group) of the longest groups scored by a long-entry kernel (view 0) */
     char long_kernel[24];    /* that kernel: "long16_rl<R>" (packed 16-bit SW), "long32_w<W>_rl<R>" (int32;
                                 "+"-joined when split over two launches), "" none */
+    uint32_t part_retries;   /* searches run again without strip parts because a part's wait for its
+                                group's first part ran into option "part_wait_us" (results unaffected) */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -106,6 +108,12 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        strips (all groups' first parts, then all second parts),
  *                        so the launch ends on small units: 0 (default) for groups of
  *                        at least 4 strips, 1 never, 2 always
+ *   "rescore32" 1|0      entries the DP kernels cannot score exactly (overflow) are re-scored
+ *                        by the int32 long-entry kernel, one wave per entry, whenever int32 is
+ *                        exact for the DB (default); 0: always the int64 kernel
+ *   "part_wait_us" N     bound of a strip part's wait for its group's first part (default
+ *                        2000000); a timed-out wait makes the search run again without parts
+ *                        (stats part_retries), results unchanged
  *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
  *                        m_run's INFO line): -1 (default) only at output mode
  *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always

@@ -109,6 +109,8 @@ void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPl
     S.strip_rows = sc.empty() ? 0 : sc[0].strip_rows;
     S.long_entries = sc.empty() ? 0 : sc[0].long_entries;
     snprintf(S.long_kernel, sizeof S.long_kernel, "%s", sc.empty() ? "" : sc[0].long_kernel);
+    S.part_retries = 0;
+    for (const SearchScores& x : sc) S.part_retries += x.part_retries;
 }
 
 void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {
@@ -423,6 +425,8 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "pair_parts")) cfg().pair_parts = (int)value;
     else if (!strcmp(name, "batch_fuse")) cfg().batch_fuse = (int)value;
     else if (!strcmp(name, "counters")) cfg().counters = (int)value;
+    else if (!strcmp(name, "part_wait_us")) cfg().part_wait_us = std::max(0L, value);
+    else if (!strcmp(name, "rescore32")) cfg().rescore32 = (int)value;
     else print_warning("unknown option %s", name);
 }
 
@@ -469,7 +473,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         std::iota(ord.begin(), ord.end(), (size_t)0);
         std::stable_sort(ord.begin(), ord.end(),
                          [&](size_t x, size_t y) { return qviews[x][0].len < qviews[y][0].len; });
-        uint32_t launches = 0;
+        uint32_t launches = 0, retries = 0;
         for (size_t b0 = 0; b0 < nq; b0 += kMaxBatchPipe) {
             const size_t b1 = std::min(nq, b0 + kMaxBatchPipe);
             std::vector<QueryView> vs;
@@ -481,6 +485,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
                 run_search(queries[qi], al, hitcount, bit_width, false, R);
                 kms += stats().kernel_ms;
                 cells += stats().cells;
+                retries += stats().part_retries;
                 launches++;
                 const size_t n = std::min(hitcount, R.hits.size());
                 for (size_t j = 0; j < n; j++) {
@@ -495,6 +500,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
             std::vector<SearchScores> sc;
             device_search(D, vs, al, hitcount, bit_width, agg, &sc);
             kms += agg.kernel_ms;
+            retries += agg.part_retries;
             launches += agg.fused_views ? 1u : (uint32_t)vs.size();
             for (size_t bi = b0; bi < b1; bi++) {
                 const size_t i = ord[bi];
@@ -516,6 +522,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         S.kernel_ms = kms;
         S.cells = cells;
         S.kernel_launches = launches;
+        S.part_retries = retries;
         S.search_ms = now_ms() - t0;
         return total;
     }

@@ -46,6 +46,9 @@ struct Config {
                                           // 0 auto (groups of >= 4 strips), 1 whole groups, 2 always
     int batch_fuse = 1;                   // ssa_amd_search_batch: queries of one pair-kernel plan in one launch
     int pair_ticket = 1;                  // pair_kernel workgroups take groups in start order (StripArgs::ticket)
+    int rescore32 = 1;                    // overflowed lanes re-scored in int32 (long_kernel list mode) when exact
+    long part_wait_us = 2000000;          // bound of a strip part's wait for its group's first part (then the
+                                          // search runs again without parts; never a hang, never fatal)
     int timeline = 0;                     // record the DP waves' start/end (ssa_amd_get_timeline)
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always

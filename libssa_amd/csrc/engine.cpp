@@ -47,7 +47,9 @@ void DeviceDB::release() {
     if (device >= 0) check(hipSetDevice(device), "hipSetDevice");
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
-    dfree(d_work); dfree(d_order); dfree(d_lscratch);
+    dfree(d_work); dfree(d_order); dfree(d_lscratch); dfree(d_rscratch);
+    d_rscratch = nullptr;
+    rscratch_cap = 0;
     dfree(d_flags); dfree(d_flist); dfree(d_cnt); dfree(d_res_cls); dfree(d_frlist); dfree(d_frwork);
     d_frlist = nullptr; d_frwork = nullptr; frwork_cap = 0;
     dfree(d_hmm);
@@ -464,15 +466,21 @@ std::vector<SlotPlan> device_plan() {
     static std::vector<SlotPlan> plan;
     if (gen == C.db_generation && devs == C.devices && chunk == C.chunk_size && cnt == count) return plan;
     const size_t n = C.devices.size();
-    std::vector<uint64_t> lens(count, 0);
+    // one residue sum per chunk_size chunk (the cuts fall on chunk
+    // boundaries anyway): 8 B per chunk, not per record (50 M records would
+    // otherwise hold 400 MB of lengths for the duration of the cut)
+    const size_t cs = std::max<size_t>(C.chunk_size, 1);
+    const size_t nch = (count + cs - 1) / cs;
+    std::vector<uint64_t> sums(nch, 0);
     for (size_t i = 0; i < count; i++) {
         p_seqinfo si = ssa_db_get_sequence(i);
-        if (si) lens[i] = si->seqlen;
+        if (si) sums[i / cs] += si->seqlen;
     }
     std::vector<size_t> bounds(n + 1);
-    ssa_amd_shard_bounds(lens.data(), count, n, C.chunk_size, bounds.data());
+    ssa_amd_shard_bounds(sums.data(), nch, n, 1, bounds.data());
     plan.clear();
-    for (size_t s = 0; s < n; s++) plan.push_back({C.devices[s], bounds[s], bounds[s + 1]});
+    for (size_t s = 0; s < n; s++)
+        plan.push_back({C.devices[s], std::min(count, bounds[s] * cs), std::min(count, bounds[s + 1] * cs)});
     gen = C.db_generation;
     devs = C.devices;
     chunk = C.chunk_size;
@@ -737,6 +745,25 @@ static uint32_t strip_parts(uint32_t T) {
 
 // long_kernel at 4 waves per entry: rows per lane for an m-row query
 static int long_rl4(size_t m) { return m <= 512 ? 2 : m <= 768 ? 3 : 4; }
+// ... at one wave per entry
+static int long_rl1(size_t m) { return m <= 256 ? 4 : m <= 512 ? 8 : m <= 576 ? 9 : m <= 768 ? 12 : 16; }
+
+// The exact int32 re-score tier (kernels.h LongArgs::list): the DP kernels'
+// overflowed lanes are re-scored by long_kernel (one wave per entry, the
+// reference's recurrences in int32) instead of wide_kernel (one thread per
+// entry, int64, its H/E column in HBM) whenever int32 is exact for every
+// entry of the DB: R, Q <= 0 (its SW clamps E and F at 0), the profile fits
+// its int16 LDS table, and (m + n + 2)(max|M| + |Q| + |R|) < 2^30 for the
+// longest entry n (long_plan's bound).  Returns the rows per lane, or 0.
+static int rescore32_rl(const DeviceDB& D, size_t m, uint32_t A, int Q, int R, int64_t minM, int64_t maxM) {
+    const Config& C = cfg();
+    if (!C.rescore32 || C.force_wide || Q > 0 || R > 0 || A > 31 || D.len_sorted.empty() || m == 0) return 0;
+    if (minM < -32768 || maxM > 32767) return 0;
+    const int64_t amp = std::max(std::abs(minM), std::abs(maxM)) + std::abs((int64_t)Q) + std::abs((int64_t)R);
+    if ((int64_t)(m + D.len_sorted.back() + 2) * amp >= (1ll << 30)) return 0;
+    return long_rl1(m);
+}
+constexpr uint32_t kRescoreBlocks = 1024;    // the tier's grid: 4 workgroups per CU, looping over the list
 
 // long16_kernel (SW long entries on packed 16-bit patterns): the pattern of
 // score 0 -- high enough that h + Q + R and E + R never borrow across the
@@ -746,7 +773,12 @@ static int long_rl4(size_t m) { return m <= 512 ? 2 : m <= 768 ? 3 : 4; }
 // SW score) beyond the patterns' finite range (kernels.hip long16_kernel)
 static uint32_t long16_base(int Q, int R) { return 0x0400u + (uint32_t)std::max(0, -(Q + R)); }
 static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM) {
-    if (nw || !cfg().long16 || Q > 0 || R > 0 || Q + R < -16384 || minM < -32768 || D.len_sorted.empty()) return 0;
+    // (minM: a diagonal sum hd + M, hd >= base16, must stay a positive
+    // pattern; a matrix value below -base16 could wrap it into the NaN
+    // patterns 0xFC01..0xFFFF, which the maxima propagate)
+    if (nw || !cfg().long16 || Q > 0 || R > 0 || Q + R < -16384 || minM < 1 - (int64_t)long16_base(Q, R) ||
+        D.len_sorted.empty())
+        return 0;
     const int64_t mp = std::max<int64_t>(maxM, 0);
     const int64_t hmax = (int64_t)std::min<size_t>(m, D.len_sorted.back()) * mp;
     if ((int64_t)long16_base(Q, R) + hmax + mp > 0x7BFF) return 0;
@@ -958,8 +990,13 @@ bool batch_pipelinable(size_t nqueries, size_t k) {
     return nqueries > 1 && k > 0 && k <= (size_t)kFilterMaxK && !cfg().no_filter;
 }
 
-void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out,
-                   std::vector<SearchScores>* indep) {
+// One search (device_search below).  no_parts: every group as one work unit
+// (StripArgs::nparts = 1).  Returns false when a strip part's wait for its
+// group's first part ran into its bound (StripArgs::part_wait): the scores
+// of that launch are not used and the caller runs the search again without
+// parts.
+static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw,
+                               SearchScores& out, std::vector<SearchScores>* indep, bool no_parts) {
     check(hipSetDevice(D.device), "hipSetDevice");
     const Config& C = cfg();
     const size_t E = D.meta.size();
@@ -1036,7 +1073,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             check(hipMalloc((void**)&D.d_scores, V * E * 4), "scores");
             D.scores_cap = V * E;
         }
-        while (D.vev.size() < 2 * V) {
+        while (D.vev.size() < 2 * V + 1) {
             hipEvent_t e;
             check(hipEventCreate(&e), "hipEventCreate");
             D.vev.push_back(e);
@@ -1422,6 +1459,38 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             w.zero2[1] = D.d_frlist;
         }
 
+        // the int32 re-score tier for this view's overflowed lanes, when exact
+        const int rl32 = rescore32_rl(D, m, A, Q, R, minM, maxM);
+        LongArgs ra{};
+        if (rl32 > 0) {
+            w.zero_only = 1;                       // wide_kernel only clears the counters
+            ra.res = dres;
+            ra.groups = D.d_groups;
+            ra.lane_len = D.d_lane_len;
+            ra.lane_out = D.d_lane_out;
+            ra.query = D.d_query;
+            ra.matrix = D.d_matrix;
+            ra.m = (uint32_t)m;
+            ra.alpha = A;
+            ra.gap_open = Q;
+            ra.gap_extend = R;
+            ra.list = ovf + 1;
+            ra.list_count = ovf;
+            ra.list_out = wide;
+            ra.nseq = (uint32_t)ovf_capv;
+            ra.blocks = (uint32_t)std::min<size_t>(kRescoreBlocks, (ovf_capv + kLongWaves - 1) / kLongWaves);
+            if (m > (size_t)64 * rl32) {
+                ra.stride = D.group_ncols[0] + 16;
+                const size_t need = (size_t)ra.blocks * kLongWaves * ra.stride;
+                if (D.rscratch_cap < need) {
+                    if (piped && v > 0) check(hipStreamSynchronize(D.stream), "sync");
+                    dfree(D.d_rscratch);
+                    check(hipMalloc((void**)&D.d_rscratch, need * 8), "re-score scratch");
+                    D.rscratch_cap = need;
+                }
+                ra.scratch = D.d_rscratch;
+            }
+        }
         kname = use_pair ? (nw ? "pair_f16_nw" : "pair_f16_sw")
                          : use_f16 ? "strip_f16m_sw" : (nw ? "strip16_nw" : "strip16_sw");
         if (nmax16 == 0) kname = "wide_i64";
@@ -1506,7 +1575,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             // wave of W waves x 64 lanes x RL rows per pass; waves past the
             // query idle): q = 513 computes 576 rows at RL 3, 768 at RL 4
             const int rl4 = long_rl4(m);
-            const int rl1 = m <= 256 ? 4 : m <= 512 ? 8 : m <= 576 ? 9 : m <= 768 ? 12 : 16;
+            const int rl1 = long_rl1(m);
             if (rl16 > 0 ? m > (size_t)64 * rl16 : (m > (size_t)4 * 64 * rl4 || m > (size_t)64 * rl1)) {
                 la.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)long_groups * 64 * la.stride;
@@ -1572,7 +1641,12 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
             ta.zero = ovf;
-            if (C.pair_ticket) ta.zero_ticket = gate + 1;
+            // the start-order ticket (StripArgs::ticket): always with strip
+            // parts, whose waits rely on it
+            {
+                const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
+                if (C.pair_ticket || (!no_parts && strip_parts(T) > 1)) ta.zero_ticket = gate + 1;
+            }
             if (long_groups > 0) {
                 // (at most what can be resident at once: every long workgroup
                 // pads its LDS to the pair table's size, so a CU holds
@@ -1630,7 +1704,7 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (!fused || v + 1 == V) {
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 const size_t nqf = fused ? V : 1;
-                uint32_t parts = strip_parts(T);
+                uint32_t parts = no_parts ? 1u : strip_parts(T);
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
                     const uint32_t ps = (T + parts - 1) / parts;
@@ -1655,6 +1729,11 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                     b.part_done = D.d_part;
                     b.part_smax = D.d_smax;
                     b.part_err = gate + 2;
+                    // (ticks of the 100 MHz s_memrealtime clock)
+                    b.part_wait = (uint32_t)std::min<uint64_t>(0xffffffffull, (uint64_t)C.part_wait_us * 100);
+                    // a part waits only for a unit that holds an earlier
+                    // start-order ticket, i.e. one already resident or done
+                    b.ticket = gate + 1;
                     if (fused) {
                         b.rowbuf2 = (uint4*)(D.d_rowbuf_q + nqf * (size_t)D.nblocks * 4096);
                     } else {
@@ -1694,6 +1773,9 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 }
                 b.paddr = D.d_paddr;
             }
+            // a fused batch's DP time runs from this one launch (not from view
+            // 0's start: the host prepared the other views in between)
+            if (fused && v + 1 == V) check(hipEventRecord(D.vev[2 * V], st), "event");
             if (!fused || v + 1 == V)
                 check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
@@ -1706,7 +1788,8 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
             if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
             if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
             check(hipEventRecord(ev_k1, st), "event");
-            check(launch_wide(w, wide_threads, st), "wide kernel launch");
+            check(launch_wide(w, rl32 > 0 ? 64u : wide_threads, st), "wide kernel launch");
+            if (rl32 > 0) check(launch_long(ra, 1, rl32, nw, st), "int32 re-score launch");
             if (want_counts) {
                 // 8/16-bit overflow flags of this view's lanes (counters.hip);
                 // "ordinary" widths are decided from exact values and bounds
@@ -1731,8 +1814,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
                 fa.entry_lane = (const uint2*)D.d_entry_lane;
                 fa.entries = (uint32_t)E;
                 fa.scores = a.scores;
-                fa.query = D.d_query;
-                fa.matrix = D.d_matrix;
+                // this view's own uploads (D.d_query / D.d_matrix name the
+                // last view's when a fused batch runs its posts deferred)
+                fa.query = w.query;
+                fa.matrix = w.matrix;
                 fa.padrow = (const int64_t*)(dup + 8192);
                 fa.flags = D.d_flags + v * E;
                 fa.list = D.d_flist;
@@ -1887,7 +1972,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         const double t_sync0 = now_ms();
         check(hipStreamSynchronize(st), "search");
         sync_wait += now_ms() - t_sync0;
-        if (parts_used && *h_perr) fatal("pair kernel: a strip part waited more than 0.5 s for its predecessor");
+        // a strip part gave up waiting for its group's first part: this
+        // launch's scores are incomplete -- the caller runs the search again
+        // without parts (never fatal: a slow predecessor is a timing event)
+        if (parts_used && *h_perr) return false;
         const double t_post0 = now_ms();
 
         {
@@ -1981,8 +2069,10 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
         }
         float t;
         if (fused) {
-            // one launch for all views: from the first view's start to its end
-            check(hipEventElapsedTime(&t, D.vev[0], D.vev[2 * V - 1]), "elapsed");
+            // one launch for all views: from that launch to the join of the DP
+            // kernels (view 0's post, the first to run after it; the long-entry
+            // kernels started with their views and overlap the host's preparation)
+            check(hipEventElapsedTime(&t, D.vev[2 * V], D.vev[1]), "elapsed");
             kms += t;
             for (size_t vv = 0; vv < V; vv++) (*indep)[vv].kernel_ms = t / V;
         } else if (piped) {
@@ -2034,6 +2124,20 @@ void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, s
     out.long_entries = lentries;
     memcpy(out.long_kernel, lkname, sizeof lkname);
     out.fused_views = fused ? (uint32_t)V : 0u;
+    return true;
+}
+
+void device_search(DeviceDB& D, const std::vector<QueryView>& views, int algo, size_t k, int bw, SearchScores& out,
+                   std::vector<SearchScores>* indep) {
+    if (device_search_once(D, views, algo, k, bw, out, indep, false)) {
+        out.part_retries = 0;
+        return;
+    }
+    // (every stream of the search has been synchronised; the counters and
+    // the wait flag are zeroed again at the start of the search)
+    if (!device_search_once(D, views, algo, k, bw, out, indep, true))
+        fatal("pair kernel: strip-part wait timed out with strip parts off");
+    out.part_retries = 1;
 }
 
 }  // namespace ssa

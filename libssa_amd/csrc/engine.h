@@ -114,6 +114,8 @@ struct DeviceDB {
     hipStream_t stream_long1 = nullptr;   // long_kernel, 1 wave per entry (event ev[6])
     int64_t* d_lscratch = nullptr;
     size_t lscratch_cap = 0;              // int64 elements
+    int64_t* d_rscratch = nullptr;        // the int32 re-score tier's multi-pass rows (LongArgs::list)
+    size_t rscratch_cap = 0;              // int64 elements
     std::vector<uint32_t> lane_out;       // host copy for overflow mapping
     std::vector<uint32_t> len_sorted;     // entry lengths, ascending
     // residues are stored in a compact alphabet: device code c < alpha stands
@@ -174,6 +176,7 @@ struct SearchScores {
     uint32_t long_entries = 0;           // entries the long-entry kernels scored (view 0)
     char long_kernel[24] = {};           // which (ssa_amd_stats_t::long_kernel)
     uint32_t fused_views = 0;            // views one fused pair_kernel launch scored (0: not fused)
+    uint32_t part_retries = 0;           // 1: a strip-part wait timed out, the search ran again without parts
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;

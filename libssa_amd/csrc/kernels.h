@@ -73,7 +73,8 @@ struct StripArgs {
     uint32_t nparts, part_strips, nquads;
     uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)
     uint32_t* part_smax;       // [ngroups * 64]
-    uint32_t* part_err;        // set when a wait timed out (the host then refuses the result)
+    uint32_t* part_err;        // set when a wait timed out (the host then runs the search again without parts)
+    uint32_t part_wait;        // bound of that wait, s_memrealtime ticks (100 MHz)
     uint4* rowbuf2;            // part 1's own strip boundaries (same layout as rowbuf)
     // pair_kernel: several queries of one plan in one launch (a batch of
     // short queries, ssa_amd_search_batch): unit order part, quad (longest
@@ -123,6 +124,16 @@ struct LongArgs {
     // long16_kernel (SW on 16-bit patterns): pattern of score 0, and the
     // padding profile value (int16 in the low half)
     uint32_t base16, pad16;
+    // long_kernel (W = 1) as the exact int32 re-score tier of the DP kernels'
+    // overflowed lanes (engine.cpp): when `list` is set the entries are the
+    // lanes list[0 .. min(*list_count, nseq)), in a grid of `blocks`
+    // workgroups that loops over them; entry i's exact score goes to
+    // list_out[i] (the int64 slot wide_kernel would fill), its multi-pass
+    // scratch row is its wave's slot
+    const uint32_t* list;
+    const uint32_t* list_count;
+    int64_t* list_out;
+    uint32_t blocks;
 };
 constexpr int kLongWaves = 4;
 
@@ -143,6 +154,7 @@ struct WideArgs {
     uint32_t* zero;            // nzero dwords cleared by block 0 (the next filter pass's counters)
     uint32_t nzero;
     uint32_t* zero2[2];        // and these two dwords (the overflow-flag replay lists' counts), if set
+    uint32_t zero_only;        // 1: only the clearing above (the int32 tier, long_kernel, re-scores the list)
 };
 
 // Device-side top-k candidate filter (single query view, k <= kFilterMaxK).

@@ -384,6 +384,7 @@ strip_f16m_kernel(const StripArgs a) {
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
     if (blockIdx.x == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x >= 62 && a.zero2[threadIdx.x - 62]) *a.zero2[threadIdx.x - 62] = 0;
+    if (a.zero_only) return;
     const uint32_t n = min(*a.ovf_count, a.ovf_cap);
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -792,13 +793,18 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t wr = wave % W;                    // rank of the wave inside its entry
-    const uint32_t s = blockIdx.x * EPW + wave / W;  // entry: lane seq0 + s of the group order
-    const bool active = s < a.nseq;
-    const uint32_t ss = a.seq0 + (active ? s : 0);
+    // the re-score tier (LongArgs::list): the workgroup loops over the list,
+    // EPW entries at a time (uniform per workgroup: every wave meets the same
+    // barriers); otherwise one round, entries seq0 + s of the group order
+    const uint32_t cnt = a.list ? min(*a.list_count, a.nseq) : a.nseq;
+    for (uint32_t bi = blockIdx.x; !a.list || bi * EPW < cnt; bi += a.blocks) {
+    const uint32_t s = bi * EPW + wave / W;
+    const bool active = s < cnt;
+    const uint32_t ss = a.list ? a.list[active ? s : bi * EPW] : a.seq0 + (active ? s : 0);
     const GroupDesc gd = a.groups[ss >> 6];
     const uint32_t n = active ? a.lane_len[ss] : 0;
     const uint4* rp = a.res + (size_t)gd.blk * 64 + (ss & 63);
-    int64_t* scr = a.scratch + (size_t)ss * a.stride;
+    int64_t* scr = a.scratch + (size_t)(a.list ? blockIdx.x * EPW + wave / W : ss) * a.stride;
     const int32_t Q = a.gap_open, R = a.gap_extend, QR = Q + R;
     const uint32_t m = a.m, prow = a.alpha + 1;
     const uint32_t npass = (m + RP - 1) / RP;
@@ -1069,7 +1075,10 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
 #pragma unroll
                 for (int r = 1; r < RL; r++) hs = (rr % RL == (uint32_t)r) ? H[r] : hs;
                 score = __builtin_amdgcn_readlane(hs, rr / RL);
-                if (lane == 0) a.scores[a.lane_out[ss]] = score;
+                if (lane == 0) {
+                    if (a.list) a.list_out[s] = score;
+                    else a.scores[a.lane_out[ss]] = score;
+                }
             }
         }
     }
@@ -1080,13 +1089,21 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
         if (active && wr == 0 && lane == 0) {
             int32_t best = 0;
             for (int k = 0; k < W; k++) best = max(best, wmax[wave + k]);
-            const uint32_t o = a.lane_out[ss];
-            if (o != 0xffffffffu) a.scores[o] = best;
+            if (a.list) {
+                a.list_out[s] = best;
+            } else {
+                const uint32_t o = a.lane_out[ss];
+                if (o != 0xffffffffu) a.scores[o] = best;
+            }
         }
     } else {
         if (active && wr == 0 && lane == 0 && n == 0) {
-            const uint32_t o = a.lane_out[ss];
-            if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
+            if (a.list) {
+                a.list_out[s] = Q + (int64_t)m * R;
+            } else {
+                const uint32_t o = a.lane_out[ss];
+                if (o != 0xffffffffu) a.scores[o] = Q + (int32_t)m * R;
+            }
         }
         if (TRK) {
             for (int x = 32; x > 0; x >>= 1) {
@@ -1110,6 +1127,11 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     }
     if (a.timeline && active && wr == 0 && lane == 0)
         a.timeline[ss] = make_uint4(0x80000000u | ss, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());
+    if (!a.list) break;
+    // (the next entries' nmax, profile and maxima reuse the shared arrays:
+    // every wave is past their last reads)
+    __syncthreads();
+    }
 }
 
 #undef LONG_ISSUE
@@ -1127,8 +1149,10 @@ static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
     const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW, TRK>, attr, (int)kDynMax);
     if (e != hipSuccess) return e;
     constexpr int EPW = kLongWaves / W;
-    const uint32_t blocks = (a.nseq + EPW - 1) / EPW;
-    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
+    if (a.list && (W != 1 || a.blocks == 0 || a.hmm || a.timeline || a.gate)) return hipErrorInvalidValue;
+    LongArgs b = a;
+    if (!a.list) b.blocks = (a.nseq + EPW - 1) / EPW;
+    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(b.blocks), dim3(64 * kLongWaves), bytes, st, b);
     return hipGetLastError();
 }
 
@@ -1182,9 +1206,12 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
 // Absolute frame: value v is the pattern v + a.base16 (SW scores >= 0, so
 // every H, E, F is >= base16 >= 0x0400: E and F are clamped at the floor as
 // long_kernel clamps them at 0, exact for R <= 0).  The host
-// (engine.cpp long16_plan) checks base16 + min(m, n) maxM + maxM <= 0x7BFF,
-// so no real value or intermediate reaches the inf/NaN patterns, and picks
-// base16 >= 0x0400 - (Q + R) so h + Q + R cannot borrow across the halves.
+// (engine.cpp long16_plan) checks base16 + min(m, n) maxM + maxM <= 0x7BFF
+// (no real value reaches the inf patterns from above) and minM > -base16
+// (a diagonal sum hd + M of a real cell stays a positive pattern: it cannot
+// wrap into the NaN patterns 0xFC01..0xFFFF, which the maxima would
+// propagate), and picks base16 >= 0x0400 - (Q + R) so h + Q + R cannot
+// borrow across the halves.
 // Padding (rows past the query, the padding code of columns past an entry)
 // scores a.pad16 = maxM - 32767: hd + pad16 wraps to a negative f16 pattern
 // in [0x8001, 0xFC00], which every maximum drops, so a padding cell's H is

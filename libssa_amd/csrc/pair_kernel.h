@@ -142,13 +142,15 @@ pair_kernel(const StripArgs a) {
         if (part > 0) {
             // the group's previous part must be done: its strip boundary rows
             // (row buffer) and running maxima come from that workgroup.  Its
-            // unit had a lower ticket, so it is resident or finished: the wait
-            // ends (bounded anyway -- a timeout is reported, never a hang)
+            // unit had a lower start-order ticket (tickets are always on with
+            // parts), so it is resident or finished: the wait ends.  Bounded
+            // anyway (a.part_wait): a timeout is reported and the host runs
+            // the search again without parts -- never a hang
             if (threadIdx.x == 0) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (__hip_atomic_load(a.part_done + (size_t)wg * nqs + qi, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) < part) {
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {       // 0.5 s
+                    if (__builtin_amdgcn_s_memrealtime() - t0 >= a.part_wait) {
                         __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
                     }

@@ -273,20 +273,26 @@ def to_ascii(codes: np.ndarray, nucleotide: bool = False) -> np.ndarray:
 
 def write_fasta(path: str, codes: np.ndarray, off: np.ndarray, nucleotide: bool = False,
                 line: int = 0) -> None:
-    """Writes one record per sequence ('>i' header, sequence on one line)."""
-    asc = to_ascii(codes, nucleotide)
+    """Writes one record per sequence ('>i' header, sequence on one line).
+    Vectorised per block of records: each block's residues are converted
+    at once and the "\\n>i\\n" separators inserted at the record starts
+    (np.insert), so a 10 M-sequence DB takes seconds, not minutes."""
+    table = np.frombuffer((NT_ORDER if nucleotide else AA_ORDER).encode(), dtype=np.uint8)
     n = len(off) - 1
+    off = np.asarray(off, dtype=np.int64)
     with open(path, "wb", buffering=1 << 24) as f:
-        # build in blocks to bound memory
         blk = 65536
         for b0 in range(0, n, blk):
             b1 = min(n, b0 + blk)
-            parts = []
-            for i in range(b0, b1):
-                parts.append(b">%d\n" % i)
-                parts.append(asc[int(off[i]):int(off[i + 1])].tobytes())
-                parts.append(b"\n")
-            f.write(b"".join(parts))
+            heads = [b">%d\n" % i for i in range(b0, b1)]
+            # record r's insert: the previous record's newline (r > b0), its header
+            ilen = np.fromiter((len(h) + 1 for h in heads), dtype=np.int64, count=b1 - b0)
+            ilen[0] -= 1
+            r0, r1 = int(off[b0]), int(off[b1])
+            out = np.insert(table[codes[r0:r1]], np.repeat(off[b0:b1] - r0, ilen),
+                            np.frombuffer(b"\n".join(heads), dtype=np.uint8))
+            f.write(out.tobytes())
+            f.write(b"\n")
 
 
 def query_string(codes: np.ndarray, nucleotide: bool = False) -> str:

@@ -224,13 +224,15 @@ MODE_SEARCH8_AVX2 = 7
 
 def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_open: int = 0,
             gap_extend: int = 0, k: int = 10, chunk: int = 1000, threads: int = 1, repeat: int = 1,
-            db_off=None, views=None, chunk_counts=False):
+            db_off=None, views=None, chunk_counts=False, raw_hits=False):
     """Runs the reference harness.  Returns raw per-seq scores (mode 0), the
     tables blob (mode 4), or (hits, overflow_count, nseq, seconds) for the
     searches -- overflow_count is the 16-bit count, or (o8, o16) for the
     8-bit mode 7; with chunk_counts the per-chunk [nchunks, 2] (o8, o16)
     array is appended.  views: a list of equal-length query views (searched
-    as one multi-view query) instead of `query`."""
+    as one multi-view query) instead of `query`.  raw_hits: the hits as an
+    int64 [count, 2] (score, id) array instead of a list of tuples (the
+    multi-million-hit full-size fixtures)."""
     nviews = 0
     if views is not None:
         nviews = len(views)
@@ -289,7 +291,7 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
         return mats, maps
     cnt = struct.unpack_from("<Q", data, 0)[0]
     arr = np.frombuffer(data, dtype=np.int64, count=2 * cnt, offset=8).reshape(cnt, 2)
-    hits = [(int(a), int(b)) for a, b in arr]
+    hits = arr.copy() if raw_hits else [(int(a), int(b)) for a, b in arr]
     pos = 8 + 16 * cnt
     ovf, ns = struct.unpack_from("<QQ", data, pos)
     secs = struct.unpack_from("<d", data, pos + 16)[0]

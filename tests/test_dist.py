@@ -291,6 +291,58 @@ def test_bench_launcher_spawns_ranks(world):
     assert all(x["launcher"] == "bench.py --gpus" for x in d["ranks"])
 
 
+@pytest.mark.parametrize("world,visible,rehearsal", [(2, 1, True), (3, 1, True), (2, 8, False), (8, 8, False)])
+def test_bench_rank_layout_labels_rehearsals(world, visible, rehearsal):
+    """Every rank derives the same layout from the world size and the
+    visible GPU count: a gloo run with more ranks than GPUs says
+    "rehearsal" and counts physical GPUs in n_gpus (it never claims N GPUs
+    for one GPU's work); one rank per GPU is not a rehearsal."""
+    import json
+    r = _bench(["--gpus", str(world), "--launch-selftest"],
+               env_extra={"SSA_DIST_BACKEND": "gloo", "SSA_BENCH_VISIBLE_GPUS": str(visible)})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    lay = [x["layout"] for x in d["ranks"]]
+    assert all(x["n_gpus"] == min(world, visible) for x in lay)
+    assert [x["device"] for x in lay] == [r % visible for r in range(world)]
+    if rehearsal:
+        assert all(x["ranks_per_gpu"] == -(-world // visible) for x in lay)
+        assert all(x["rehearsal"] == f"{world} ranks on {visible} GPU(s), exchange over gloo" for x in lay)
+    else:
+        assert all(x["ranks_per_gpu"] == 1 and "rehearsal" not in x for x in lay)
+
+
+def test_rank_layout_refuses_doubling_up_without_gloo():
+    from libssa_amd import workloads as W
+    assert W.rank_layout(1, 0, 0, "nccl") == (0, 1, 1)
+    assert W.rank_layout(4, 8, 3, "nccl") == (3, 1, 4)
+    assert W.rank_layout(4, 2, 3, "gloo") == (1, 2, 2)
+    with pytest.raises(SystemExit):
+        W.rank_layout(4, 2, 3, "nccl")
+
+
+def test_workload_cuts_balance_and_cover():
+    """The cut bench.py and the GPU tests share (libssa_amd/workloads.py):
+    weak configs N x seqs IDs, strong ones the fixed DB; protein slices
+    balanced by residues, contiguous, covering the job."""
+    from libssa_amd import synthetic as syn
+    from libssa_amd import workloads as W
+    cfg = W.CONFIGS["north_star"]
+    q = W.query(cfg)
+    b, total, job = W.cuts(cfg, 4, q, seqs=None)
+    assert total == job == 10_000_000 and b[0] == 0 and b[-1] == job and b == sorted(b)
+    lens = syn.protein_lengths_range(total, 42, 0, job, query=q)
+    res = [int(lens[x:y].sum()) for x, y in zip(b, b[1:])]
+    assert max(res) / min(res) <= 1.001
+    b2, total2, job2 = W.cuts(W.CONFIGS["c2"], 2, q, seqs=1000)
+    assert (total2, job2) == (2000, 2000) and b2[0] == 0 and b2[-1] == 2000
+    b5, total5, job5 = W.cuts(W.CONFIGS["c5"], 8, W.query(W.CONFIGS["c5"]))
+    assert total5 == job5 == 50_000_000 and b5 == [r * 6_250_000 for r in range(9)]
+    # a per-rank share of a strong config: cut by count (the c4 fixture's first share)
+    b4, _, job4 = W.cuts(W.CONFIGS["c4"], 2, q, seqs=1_250_000)
+    assert b4 == [0, 1_250_000, 2_500_000] and job4 == 2_500_000
+
+
 def test_bench_launcher_propagates_failure():
     """A rank that dies takes the job down: the parent stops the others
     (which wait in the rendezvous for it) and exits with that rank's status."""

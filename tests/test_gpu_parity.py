@@ -403,6 +403,49 @@ def test_strip_parts_keep_scores(algo, qlen):
         S.free_sequence(qq)
 
 
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_strip_part_wait_timeout_reruns_without_parts(algo):
+    """A strip part whose wait for its group's first part runs into its
+    bound (option "part_wait_us"; 0 here, so practically every second part
+    times out) is not fatal: the search runs again without parts, the
+    scores and top-k stay exact, and stats count the retry -- single
+    queries and a fused batch (one pair_kernel launch for several queries)."""
+    rng = np.random.default_rng(31)
+    q = syn.protein_query(300, 5)
+    lens = np.array([2000, 1500, 0] + list(rng.integers(1, 500, 6000)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        qs = [S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q[:n])) for n in (300, 290, 299)]
+        try:
+            S.set_option("pair_parts", 2)
+            S.set_option("part_wait_us", 0)
+            sc, ids = _full_scores(qq, algo, len(keep))
+            assert (ids == keep).all() and (sc == exp).all(), np.nonzero(sc != exp)[0][:10]
+            assert S.stats()["part_retries"] == 1
+            top = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
+            assert top == po.topk(exp, keep.astype(np.uint64), 10)
+            batch = S.search_batch(qs, algo, 10)
+            assert S.stats()["part_retries"] >= 1
+            S.set_option("part_wait_us", 2_000_000)
+            single = [[tuple(map(int, h[:2])) for h in S.search(x, algo, 10)] for x in qs]
+            assert [[tuple(map(int, h[:2])) for h in b] for b in batch] == single
+            assert S.stats()["part_retries"] == 0
+        finally:
+            S.set_option("pair_parts", 0)
+            S.set_option("part_wait_us", 2_000_000)
+        for x in qs + [qq]:
+            S.free_sequence(x)
+
+
 LONG_QLENS = [1, 5, 63, 64, 65, 255, 256, 257, 384, 385, 400, 512, 513, 640, 641, 768, 769, 1024, 1025, 1500, 2049]
 
 
@@ -1413,6 +1456,71 @@ def test_sharded_db_logs_merge_to_reference_topk(name, world, balanced, tmp_path
     for k in (1, 10, 64):
         got = [[int(a), int(b)] for a, b in S.merge_logs([[h for h in L] for L in logs], k)]
         assert got == c[f"top{k}"], k
+
+
+def _gather_from_threads(logs, k, group):
+    """ssa_amd_gather_logs from len(logs) host threads, each one rank of the
+    library's in-process transport (ssa_amd_dist_init_fake: the slot layout,
+    count rows and exact-size round of the RCCL path); rank 0's result."""
+    import threading
+    world = len(logs)
+    res, errs = [None] * world, []
+
+    def run(r):
+        try:
+            S.dist_init_fake(r, world, group)
+            try:
+                res[r] = S.gather_logs(logs[r], k)
+            finally:
+                S.dist_finalize()
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
+    assert all(x == [] for x in res[1:])
+    return [[int(a), int(b)] for a, b in res[0]]
+
+
+@pytest.mark.parametrize("config,world,fixture", [("c2", 4, "c2x4"), ("c2", 8, "c2x8"), ("north_star", 8, "c4full")])
+def test_driver_cuts_gather_to_reference_topk(config, world, fixture, tmp_path):
+    """Exactly what the driver's `bench.py --gpus N` searches, on one GPU:
+    the workload cut into N rank slices by libssa_amd/workloads.py (the cut
+    bench.py imports: C2's weak-scaling N M-sequence DB, and the north-star
+    10 M-sequence DB, both residue-balanced), each slice packed with its
+    global ID offset and searched at API width 16, and the real shard logs
+    gathered by ssa_amd_gather_logs from N threads over the in-process
+    transport: rank 0's top-1/10/64 equal the reference's own search of the
+    whole DB (tests/golden/fullsize.json; reference: the thread heaps merged
+    in thread order, src/algo/manager.c:141-145)."""
+    from libssa_amd import workloads as W
+    cfg = W.CONFIGS[config]
+    fx = FULL[fixture]
+    q = W.query(cfg)
+    bounds, total, job = W.cuts(cfg, world, q)
+    assert (total, job) == (fx["n"], fx["i1"])
+    configure(False, ("builtin", cfg["matrix"]), cfg["gap_open"], cfg["gap_extend"])
+    logs = []
+    try:
+        for r in range(world):
+            codes, off = W.slice_db(cfg, q, total, bounds[r], bounds[r + 1])
+            path = os.path.join(str(tmp_path), f"db{r}.fas")
+            syn.write_fasta(path, codes, off, False)
+            del codes, off
+            S.init_db(path)
+            S.set_id_offset(bounds[r])
+            S.prepare_db()
+            os.remove(path)
+            qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+            logs.append(S.search(qq, S.SW, 64, 16, S.LOG))
+            S.free_sequence(qq)
+    finally:
+        S.set_id_offset(0)
+    for k in (1, 10, 64):
+        assert _gather_from_threads(logs, k, group=7000 + 10 * world + k) == fx[f"top{k}"], k
 
 
 @pytest.mark.parametrize("gaps", [(-11, 2), (3, -1)])

@@ -10,9 +10,9 @@ run() {   # name, args...
     python -c "import json; d=json.load(open('gpurun_out/bench_all/$name.json')); c=d.get('cpu_baseline') or {}; print('$name', d['value'], d['kernel']['avg_ms'], d['kernel']['kernel_gcups'], d.get('topk_vs_reference'), c.get('value'), c.get('cores'))"
 }
 run c2 --steps 10 &&
-run c3 --config c3 --steps 5 &&
-run c4share --config c4 --seqs 1250000 --steps 10 &&
-run c5share1m --config c5 --seqs 1000000 --steps 3 --no-cpu-baseline &&
-run c5share --config c5 --seqs 6250000 --steps 2 --warmup 1 &&
-run ref --config ref --steps 5 --no-cpu-baseline &&
-run c4full --config c4 --steps 3 --warmup 1 --no-cpu-baseline
+run c3 --config c3 --steps 5 --no-north-star &&
+run c4share --config c4 --seqs 1250000 --steps 10 --no-north-star &&
+run c5share1m --config c5 --seqs 1000000 --steps 3 --no-cpu-baseline --no-north-star &&
+run c5share --config c5 --seqs 6250000 --steps 2 --warmup 1 --no-north-star &&
+run ref --config ref --steps 5 --no-cpu-baseline --no-north-star &&
+run c4full --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-north-star

@@ -301,6 +301,9 @@ FULLSIZE = {
     # one GPU's share of C5 at N = 8 (the first 6.25 M of the 50 M reads)
     "c5share8": dict(kind="dna", n=50_000_000, i1=6_250_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
                      gap_open=-4, gap_extend=-2, algo="sw", width=16),
+    # the whole 50 M-read C5 DB (7.5e9 residues, 7.5e13 cells) on one GPU
+    "c5full": dict(kind="dna", n=50_000_000, i1=50_000_000, seed=43, qlen=10_000, qseed=8, matrix="const5_-4",
+                   gap_open=-4, gap_extend=-2, algo="sw", width=16),
     "sp25": dict(kind="protein", n=500_000, i1=500_000, seed=44, qlen=400, qseed=7, matrix="blosum62",
                  gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="sprot25"),
     "u28": dict(kind="protein", n=200_000, i1=200_000, seed=45, qlen=400, qseed=7, matrix="blosum62",
@@ -359,9 +362,10 @@ def gen_fullsize(names=None):
         t0 = time.time()
         # k = n: every (score, id) stays in the reference's heap
         hits, ovf, ns, secs = po.ref_run(mode, algo, q, None, M, c["gap_open"], c["gap_extend"], k=n, threads=8,
-                                         db_off=(codes, off))
+                                         db_off=(codes, off), raw_hits=True)
+        del codes
         assert ns == n == len(hits)
-        arr = np.array(hits, dtype=np.int64)
+        arr = hits
         order = np.argsort(arr[:, 1], kind="stable")
         ids, sc = arr[order, 1], arr[order, 0]
         assert (ids == np.arange(n)).all()

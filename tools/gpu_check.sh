@@ -11,6 +11,6 @@ shift
 i=0
 for a in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 python bench.py --no-cpu-baseline $a > gpurun_out/b$i.json 2> gpurun_out/b$i.err || { tail -20 gpurun_out/b$i.err; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-north-star $a > gpurun_out/b$i.json 2> gpurun_out/b$i.err || { tail -20 gpurun_out/b$i.err; exit 1; }
   python -c "import json,sys; d=json.load(open('gpurun_out/b$i.json')); print('$a', d['value'], d['kernel']['name'], d['kernel']['avg_ms'], d['kernel']['kernel_gcups'], d['kernel']['wide_count'], d['kernel']['wide_ms_avg'], d['top_hit'], d.get('topk_vs_reference'))"
 done

@@ -12,7 +12,7 @@ REPO=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-north-star $*"
 PASSES=${PASSES:-"stats fetch write valu wait lds icache"}
 run() {   # name, rocprof args...
     local name=$1; shift

@@ -18,9 +18,23 @@ def mean_counter(d, name, kernel=None):
     return sum(vals) / len(vals)
 
 
+def bench_key(pmc_dir):
+    """The workload key bench.py printed (roofline.traffic_key) in the PMC
+    pass's own log: the traffic is filed under the exact workload profiled."""
+    for name in ("fetch.log", "write.log", "stats.log"):
+        p = os.path.join(pmc_dir, name)
+        if os.path.exists(p):
+            for line in reversed(open(p).read().splitlines()):
+                if line.startswith("{"):
+                    return json.loads(line)["roofline"]["traffic_key"]
+    raise SystemExit(f"no bench.py line under {pmc_dir}")
+
+
 def main():
-    pmc_dir, key = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[3] if len(sys.argv) > 3 else None   # substring of the dominant kernel's name
+    # usage: traffic_from_pmc.py <profile_pmc.sh out dir> [kernel name substring]
+    pmc_dir = sys.argv[1]
+    key = bench_key(pmc_dir)
+    kernel = sys.argv[2] if len(sys.argv) > 2 else None   # substring of the dominant kernel's name
     fetch = mean_counter(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE", kernel) * 1024 * 2
     write = mean_counter(os.path.join(pmc_dir, "write"), "WRITE_SIZE", kernel) * 1024
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
