@@ -665,6 +665,60 @@ def test_int16_overflow_reroute(algo):
         S.free_sequence(qq)
 
 
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_int32_rescore_tier_vs_oracle(algo):
+    """Overflowed lanes (here: the int16 strip kernel, constant 127/-1, where
+    >= 10 % of the entries -- copies of the query -- score beyond 16 bits)
+    are re-scored by the exact int32 tier (long_kernel over the overflow
+    list, one wave per entry) instead of the int64 one-thread-per-entry
+    kernel: every score equals the oracle's full_sw / full_nw, the same
+    lanes are re-scored, and the tier is far faster (reference: the
+    re-score cascade of src/algo/16/search_16.c:101-109)."""
+    rng = np.random.default_rng(17)
+    q = rng.choice(syn.AA_CODES, size=700).astype(np.uint8)
+    n = 12000
+    lens = rng.integers(20, 600, n)
+    seqs = [rng.choice(syn.AA_CODES, size=int(x)).astype(np.uint8) for x in lens]
+    for i in range(0, n, 8):                 # 1 in 8: a near-copy of the query
+        a = int(rng.integers(0, 60))
+        s = q[a:].copy()
+        s[rng.random(len(s)) < 0.02] = syn.AA_CODES[0]
+        seqs[i] = s
+    codes = np.concatenate(seqs)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    M = po.matrix_constant(127, -1)
+    exp = po.scores(algo, q, codes, off, M, -1, -1)
+    configure(False, ("const", 127, -1), -1, -1)
+    S.set_option("counters", 0)          # (timed below: no overflow-counter replays in wide_ms)
+    ms = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            S.set_option("sw_kernel", 1)
+            S.set_option("long_groups", 0)
+            for r32 in (1, 0):
+                S.set_option("rescore32", r32)
+                sc, ids = _full_scores(qq, algo, n)
+                assert (sc == exp).all(), (r32, np.nonzero(sc != exp)[0][:10])
+                st = S.stats()
+                assert st["wide_count"] >= n // 10, st["wide_count"]
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                best = []
+                for _ in range(3):
+                    assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, ids, 10)
+                    best.append(S.stats()["wide_ms"])
+                ms[r32] = min(best)
+        finally:
+            S.set_option("sw_kernel", 0)
+            S.set_option("long_groups", -1)
+            S.set_option("rescore32", 1)
+        S.free_sequence(qq)
+    print(f"re-score of {st['wide_count']} lanes: int32 tier {ms[1]:.3f} ms, int64 kernel {ms[0]:.3f} ms")
+    assert ms[0] >= 10 * ms[1], ms
+
+
 def test_shard_logs_replay_to_global_result():
     """The insertion logs of consecutive ID shards, concatenated in shard
     order and replayed, equal the single-DB top-k including tie IDs."""
@@ -1332,7 +1386,7 @@ def _fullsize_query(c):
 
 # fixtures pinned by top-k and counters only (the GPU test does not pull their
 # multi-million-entry logs through Python)
-LARGE = ("c4full", "c5share8")
+LARGE = ("c4full", "c5share8", "c5full")
 
 
 @pytest.mark.parametrize("name", sorted(k for k in FULL if k not in LARGE and not k.startswith("c2x")))
@@ -1381,11 +1435,13 @@ def test_fullsize_matches_reference_hash(name, tmp_path):
     S.free_sequence(qq)
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", [k for k in LARGE if k in FULL])
 def test_large_db_matches_reference(name, tmp_path):
     """BASELINE.json's largest single-GPU workloads at their stated size: C4's
-    whole 10 M-sequence DB (3.5e9 residues) at API width 8, and one GPU's
-    share of C5 at N = 8 (the first 6.25 M of the 50 M reads, q = 10 000 nt):
+    whole 10 M-sequence DB (3.5e9 residues) at API width 8, C5's whole 50 M
+    reads (7.5e9 residues, q = 10 000 nt: 7.5e13 cells per search) and one
+    GPU's share of C5 at N = 8 (the first 6.25 M reads):
     sw_align's top-1/10/64 and m_run's overflow counters equal the
     reference's own AVX2 search of the same DB (tests/golden/fullsize.json;
     the full score vectors' hashes are pinned on the 1.25 M / 1 M shares)."""
