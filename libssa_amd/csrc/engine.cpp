@@ -63,10 +63,10 @@ void DeviceDB::release() {
     rowbuf_q_cap = 0;
     dfree(d_rowbuf2);
     d_rowbuf2 = nullptr;
-    dfree(d_paddr);
-    d_paddr = nullptr;
-    paddr_valid = false;
-    paddr_cls.clear();
+    for (auto& pr : prs) {
+        dfree(pr.d);
+        pr = PairRows();
+    }
     dfree(d_timeline);
     d_timeline = nullptr;
     timeline_cap = timeline_rows = 0;
@@ -110,7 +110,7 @@ void DeviceDB::release() {
 }
 
 constexpr size_t kOvfPinned = 4096;      // overflow entries the pinned mirrors hold (more: pageable copies)
-// per-search device upload block: [compact matrix 8 KiB][code-0 row 256 B][top boundary][query]
+// per-search device upload block: [kernel-code matrix 8 KiB][code-0 row 256 B][top boundary][query]
 constexpr size_t kUpHeader = 8192 + 256;
 
 // ------------------------------------------------------------ entry codes
@@ -821,6 +821,9 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
 struct ViewPlan {
     std::vector<uint8_t> cls_of, cls_rep;
     bool use_cls = false;
+    // the kernels' codes' profile rows: crow[c * 32 + y] = score of kernel
+    // code c against query code y (a class's representative row)
+    std::vector<int64_t> crow;
     uint32_t A = 0, prow = 0;
     int64_t minM = 0, maxM = 0;
     uint32_t nmax16 = 0, nw_base = 0, long_groups = 0;
@@ -846,6 +849,7 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     const int64_t* M = matrix().m;
     const size_t m = qv.len;
     const size_t ml = force ? force->m : m;        // row count of the length limits
+    vp = ViewPlan();
     std::vector<uint8_t>& cls_of = vp.cls_of;
     std::vector<uint8_t>& cls_rep = vp.cls_rep;
     // residue classes of this view: DB codes whose matrix rows agree on
@@ -880,15 +884,20 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
         const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
         return std::make_pair(w, pn);
     };
-    const bool use_cls = vp.use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
-                         pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
-    const std::vector<uint8_t>& code_of = use_cls ? cls_rep : D.code_of;
-    // profile bounds over the residue codes the DB holds
-    const uint32_t A = (uint32_t)code_of.size();
+    bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
+                   pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
+    // kernel codes: the classes, or the compact codes themselves
+    uint32_t A = use_cls ? (uint32_t)cls_rep.size() : D.alpha;
+    std::vector<int64_t>& crow = vp.crow;
+    crow.assign((size_t)std::max<uint32_t>(A, 1) * 32, -1);
+    for (uint32_t c = 0; c < A; c++)
+        memcpy(&crow[(size_t)c * 32], M + ((size_t)(use_cls ? cls_rep[c] : D.code_of[c]) << 5), 32 * 8);
+    vp.use_cls = use_cls;
+    // profile bounds over the kernel codes
     int64_t minM = INT64_MAX, maxM = INT64_MIN;
     for (size_t i = 0; i < m; i++)
         for (uint32_t c = 0; c < A; c++) {
-            const int64_t x = M[(code_of[c] << 5) + qv.seq[i]];
+            const int64_t x = crow[(size_t)c * 32 + qv.seq[i]];
             minM = std::min(minM, x);
             maxM = std::max(maxM, x);
         }
@@ -1249,7 +1258,6 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         const ViewPlan& vp = vpl;
         const bool use_cls = vp.use_cls;
         const std::vector<uint8_t>& cls_of = vp.cls_of;
-        const std::vector<uint8_t>& cls_rep = vp.cls_rep;
         const uint4* dres = D.d_res;
         if (use_cls) {
             if (D.cls_key != cls_of) {
@@ -1260,14 +1268,13 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 ra.in = D.d_res;
                 ra.out = D.d_res_cls;
                 ra.n16 = D.nblocks * 64;
-                for (int c = 0; c < 64; c++) ra.map[c] = (uint8_t)cls_rep.size();   // padding / unused codes
+                for (int c = 0; c < 64; c++) ra.map[c] = (uint8_t)vp.A;   // padding / unused codes
                 for (uint32_t c = 0; c < D.alpha; c++) ra.map[c] = cls_of[c];
                 check(launch_recode(ra, D.stream), "recode launch");
                 D.cls_key = cls_of;
             }
             dres = D.d_res_cls;
         }
-        const std::vector<uint8_t>& code_of = use_cls ? cls_rep : D.code_of;
         const uint32_t A = vp.A, prow = vp.prow;
         const int64_t minM = vp.minM, maxM = vp.maxM;
         const uint32_t nmax16 = vp.nmax16, nw_base = vp.nw_base, long_groups = vp.long_groups;
@@ -1283,7 +1290,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // (the pair kernel's tables are built on the device: pair_tables_kernel)
         std::vector<uint16_t> P(use_pair ? 0 : (size_t)(A + 1) * mpad, (uint16_t)padv);
         for (uint32_t c = 0; c < (use_pair ? 0u : A); c++) {
-            const int64_t* row = M + ((size_t)code_of[c] << 5);
+            const int64_t* row = vp.crow.data() + (size_t)c * 32;
             uint16_t* pc = P.data() + (size_t)c * mpad;
             for (size_t i = 0; i < m; i++)
                 pc[i] = (uint16_t)(int16_t)std::max<int64_t>(-32768, std::min<int64_t>(32767, row[qv.seq[i]] + rel));
@@ -1306,10 +1313,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                             (uint32_t)(uint16_t)val(c, i) | ((uint32_t)(uint16_t)val(c, i + np) << 16);
                     }
         }
-        // the int64 kernel scores compact codes too
+        // the kernel codes' matrix (every kernel reads residues in kernel codes)
         int64_t Mc[1024];
         for (int x = 0; x < 32; x++)
-            for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? M[(code_of[x] << 5) + y] : -1;
+            for (int y = 0; y < 32; y++) Mc[(x << 5) + y] = (uint32_t)x < A ? vp.crow[(size_t)x * 32 + y] : -1;
         const uint32_t wide_threads = (uint32_t)(std::max<size_t>(64, std::min<size_t>(16384, (64ull << 20) / (16 * m))) / 64 * 64);
         // a multi-view search's earlier views may still be queued on the
         // stream: drain it before a device buffer they read is reallocated
@@ -1621,8 +1628,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 else if (long4 == long_groups) snprintf(lkname, sizeof lkname, "long32_w4_rl%d", rl4);
                 else snprintf(lkname, sizeof lkname, "long32_w4_rl%d+w1_rl%d", rl4, rl1);
             }
-            lds_long = std::max(pair_lds, rl16 > 0 ? long16_lds_bytes(A, rl16)
-                                                   : long4 > 0 ? long_lds_bytes(A, 4, rl4) : long_lds_bytes(A, 1, rl1));
+            lds_long = std::max(pair_lds, rl16 > 0 ? long16_lds_bytes(la.alpha, rl16)
+                                                   : long4 > 0 ? long_lds_bytes(la.alpha, 4, rl4)
+                                                               : long_lds_bytes(la.alpha, 1, rl1));
         }
         // the pair tables after the long entries' launch: long_kernel only
         // needs the uploads, so its workgroups are dispatched before the
@@ -1754,24 +1762,42 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 // plan; on this stream any earlier pair launch has finished
                 // reading it before it is rewritten)
                 const uint32_t rowB = (uint32_t)(lnp + 4) * 4;
-                if (!D.paddr_valid || D.paddr_use_cls != use_cls || D.paddr_prow != A + 1 ||
-                    D.paddr_row_bytes != rowB || (use_cls && D.paddr_cls != cls_of)) {
-                    if (!D.d_paddr) check(hipMalloc((void**)&D.d_paddr, (size_t)D.nblocks * 4096), "pair-row stream");
+                auto same = [&](const DeviceDB::PairRows& r) {
+                    return r.valid && r.use_cls == use_cls && r.prow == A + 1 && r.row_bytes == rowB &&
+                           (!use_cls || r.cls == cls_of);
+                };
+                DeviceDB::PairRows* pr = same(D.prs[0]) ? &D.prs[0] : same(D.prs[1]) ? &D.prs[1] : nullptr;
+                if (!pr) {
+                    // a free slot (the second only if a stream is at most a
+                    // quarter of the free memory), else the least recently used
+                    const size_t bytes = (size_t)D.nblocks * 2048;
+                    pr = &D.prs[0];
+                    if (D.prs[0].d) {
+                        if (!D.prs[1].d) {
+                            size_t fr = 0, tot = 0;
+                            check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
+                            if (bytes <= fr / 4) pr = &D.prs[1];
+                        } else if (D.prs[1].used < D.prs[0].used) {
+                            pr = &D.prs[1];
+                        }
+                    }
+                    if (!pr->d) check(hipMalloc((void**)&pr->d, bytes), "pair-row stream");
                     PairAddrArgs pa{};
                     pa.res = dres;
-                    pa.out = D.d_paddr;
+                    pa.out = pr->d;
                     pa.groups = D.d_groups;
                     pa.ngroups = D.ngroups;
                     pa.prow = A + 1;
                     pa.row_bytes = rowB;
                     check(launch_pair_addr(pa, st), "pair-row stream launch");
-                    D.paddr_valid = true;
-                    D.paddr_use_cls = use_cls;
-                    D.paddr_prow = A + 1;
-                    D.paddr_row_bytes = rowB;
-                    D.paddr_cls = use_cls ? cls_of : std::vector<uint8_t>();
+                    pr->valid = true;
+                    pr->use_cls = use_cls;
+                    pr->prow = A + 1;
+                    pr->row_bytes = rowB;
+                    pr->cls = use_cls ? cls_of : std::vector<uint8_t>();
                 }
-                b.paddr = D.d_paddr;
+                pr->used = ++D.pr_clock;
+                b.paddr = pr->d;
             }
             // a fused batch's DP time runs from this one launch (not from view
             // 0's start: the host prepared the other views in between)

@@ -126,13 +126,20 @@ struct DeviceDB {
     // and the class map it was made with
     uint4* d_res_cls = nullptr;
     std::vector<uint8_t> cls_key;
-    // pair_kernel's pair-row stream (StripArgs::paddr, as
-    // d_rowbuf) and what it was built from: residue copy (class map), code
-    // count + 1, row width
-    uint4* d_paddr = nullptr;
-    std::vector<uint8_t> paddr_cls;
-    bool paddr_valid = false, paddr_use_cls = false;
-    uint32_t paddr_prow = 0, paddr_row_bytes = 0;
+    // pair_kernel's pair-row streams (StripArgs::paddr, as d_rowbuf) and
+    // what each was built from: residue copy (class map), code count + 1,
+    // row width.  Two slots (the second only while memory is plentiful), so
+    // queries alternating between two strip heights (32-row strips for
+    // q <= 32 or 49..64, 48-row ones otherwise) or class maps rebuild none.
+    struct PairRows {
+        uint4* d = nullptr;
+        std::vector<uint8_t> cls;
+        bool valid = false, use_cls = false;
+        uint32_t prow = 0, row_bytes = 0;
+        uint64_t used = 0;                 // search counter at last use (LRU)
+    };
+    PairRows prs[2];
+    uint64_t pr_clock = 0;
     size_t rec_begin = 0, rec_end = 0;    // plugin records [rec_begin, rec_end) of this shard
     void release();
 };

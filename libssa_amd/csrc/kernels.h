@@ -87,10 +87,11 @@ struct StripArgs {
     uint32_t nq;
     const uint32_t* qm;
     size_t q_tab_stride, q_score_stride, q_ovf_stride, q_rowbuf_stride;
-    // pair_kernel: the pair-row stream (pair_addr_kernel), the LDS byte
-    // offset of each column's next pair row in row-buffer quads, built for
-    // this launch's table row width ((NP + 4) dwords, or (NPT + 4) when
-    // nstrips = 0) and code count
+    // pair_kernel: the pair-row stream (pair_addr_kernel), the LDS offset of
+    // each column's next pair row in 16-byte units, 16 bits per column, in
+    // octs of 8 columns (2 KiB per residue block), built for this launch's
+    // table row width ((NP + 4) dwords, or (NPT + 4) when nstrips = 0) and
+    // code count
     const uint4* paddr;
 };
 
@@ -190,6 +191,7 @@ struct FilterArgs {
 };
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 
+
 hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st);
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st);
 // a.nstrips strips of 2*np rows, then one of 2*npt rows (npt 0: none;
@@ -281,9 +283,12 @@ hipError_t launch_recode(const RecodeArgs& a, hipStream_t st);
 // pair_kernel's strips read, per column j, the LDS byte offset of the
 // pair row of column j+1, (d_{j+1} * prow + d_j) * row_bytes, from this
 // stream instead of forming it from the residue bytes (two 24-bit
-// multiplies and an add per column, ~3 % of the strip's issue time).  Same
-// layout as the row buffer: per residue block, [quad][lane][4 columns]
-// (4 KiB); the column after a group's last one takes the padding code.
+// multiplies and an add per column, ~3 % of the strip's issue time).  The
+// offset is stored in 16-byte units in 16 bits (every table row is 16-byte
+// aligned and the LDS holds at most 160 KiB): per residue block,
+// [oct][lane][8 columns] (2 KiB, half the row buffer's block) -- a shift per
+// column in the kernel for half the stream's HBM traffic; the column after
+// a group's last one takes the padding code.
 struct PairAddrArgs {
     const uint4* res;          // residue blocks (compact or class codes)
     uint4* out;                // [blocks * 256] uint4

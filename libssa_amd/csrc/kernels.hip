@@ -693,7 +693,7 @@ hipError_t launch_recode(const RecodeArgs& a, hipStream_t st) {
 
 // ------------------------------------------------------------ pair rows
 // One wave per group, one lane per sequence: each residue block's 16
-// columns become four quads of pair-row offsets (kernels.h PairAddrArgs).
+// columns become two octs of 16-bit pair-row offsets (kernels.h PairAddrArgs).
 __global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
     const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -713,11 +713,13 @@ __global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
             const uint32_t dn = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu;
             // past the group's last column: the padding code
             const uint32_t dnx = b * 16 + k + 1 < gd.ncols ? dn : pad;
-            o[k] = dnx * pairB + d * a.row_bytes;
+            o[k] = (dnx * pairB + d * a.row_bytes) >> 4;      // 16-byte units: < 2^16 for any table in LDS
         }
-        uint4* dst = a.out + (size_t)(gd.blk + b) * 256 + lane;
+        uint4* dst = a.out + (size_t)(gd.blk + b) * 128 + lane;
 #pragma unroll
-        for (int t = 0; t < 4; t++) dst[t * 64] = make_uint4(o[4 * t], o[4 * t + 1], o[4 * t + 2], o[4 * t + 3]);
+        for (int t = 0; t < 2; t++)
+            dst[t * 64] = make_uint4(o[8 * t] | o[8 * t + 1] << 16, o[8 * t + 2] | o[8 * t + 3] << 16,
+                                     o[8 * t + 4] | o[8 * t + 5] << 16, o[8 * t + 6] | o[8 * t + 7] << 16);
         cur = nxt;
     }
 }

@@ -103,6 +103,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const void* base) {
 // (aux: cache policy; the row buffer is written once and read once, so its
 // loads and stores are non-temporal: C2 +1 %, profiles/r03/stream/nt_pf_variants.txt;
 // the pair-row stream is re-read by every strip and keeps the default)
+// (w & 0xffff) << 4 in one instruction (an SDWA word select of the shifted
+// operand; left to itself the compiler emits a shift and a mask)
+__device__ __forceinline__ uint32_t lo16x16(uint32_t w) {
+    uint32_t r;
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+        : "=v"(r) : "v"(4u), "v"(w));
+    return r;
+}
 template <int AUX = 0>
 __device__ __forceinline__ uint4 load_quad(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX);
@@ -190,8 +198,10 @@ pair_kernel(const StripArgs a) {
     const uint32_t lane16 = (uint32_t)lane * 16;
     // part 0's last strip stores its boundary at device scope (the handoff)
     bool handoff = false;
-    // the pair-row stream (same block structure as the row buffer)
-    const __amdgpu_buffer_rsrc_t pap = group_rsrc(a.paddr + (size_t)gd.blk * 256);
+    // the pair-row stream: per 16-column block two octs of 64 lanes x 16 B,
+    // eight 16-bit offsets (LDS byte offset / 16) per lane and oct
+    const __amdgpu_buffer_rsrc_t pap = group_rsrc(a.paddr + (size_t)gd.blk * 128);
+    const uint32_t nocts = (nquads + 1) >> 1;
     const uint32_t gl = gg * 64 + lane;
     const uint32_t prow = a.alpha + 1;
     const uint32_t len = a.lane_len[gl];
@@ -311,20 +321,21 @@ pair_kernel(const StripArgs a) {
         uint32_t xa[2] = {0, 0};
 
         uint32_t ob[4] = {0, 0, 0, 0};
-        // row-buffer quads and the pair-row quads of the same columns,
-        // prefetched PF quads ahead (NW's shorter steps need the longer
-        // distance to cover HBM latency).  SW: two buffers used alternately
-        // (quad q in buffer q & 1; a block is four quads), so no register
-        // copies; NW: a shift register.
+        // row-buffer quads, prefetched PF quads ahead (NW's shorter steps
+        // need the longer distance to cover HBM latency).  SW: two buffers
+        // used alternately (quad q in buffer q & 1; a block is four quads), so
+        // no register copies; NW: a shift register.  The pair-row octs (eight
+        // columns) alternate between two buffers: oct 2b in ao[0] (quads 0, 1
+        // of block b), 2b + 1 in ao[1]; each is loaded two quads before use.
         constexpr int PF = NW ? 2 : 1;
         constexpr int NB = PF == 1 ? 2 : PF;
-        uint4 qn[NB], an[NB];
+        uint4 qn[NB], ao[2];
 #pragma unroll
         for (int p = 0; p < PF; p++) {
             const uint32_t nq = min((uint32_t)p, nquads - 1);
             qn[p] = load_quad<2>(qsrc, qvoff, nq * qstride);
-            an[p] = load_quad(pap, lane16, nq * 1024u);
         }
+        ao[0] = load_quad(pap, lane16, 0u);
         // P: the current column's profile operands, first the pair row
         // (d_0, pad) of column 0 (LDS byte d_0 * prow * rowB + pad * rowB);
         // the next column's row is loaded into P in place behind the row
@@ -343,23 +354,25 @@ pair_kernel(const StripArgs a) {
                 if (b * 4 + t >= nquads) break;      // uniform: the group's last columns
                 const int cb = PF == 1 ? (t & 1) : 0;
                 const uint4 qcur = qn[cb];
-                const uint4 acur = an[cb];
 #pragma unroll
-                for (int p = 0; p + 1 < PF; p++) {
-                    qn[p] = qn[p + 1];
-                    an[p] = an[p + 1];
-                }
+                for (int p = 0; p + 1 < PF; p++) qn[p] = qn[p + 1];
                 {
-                    // unconditional (past the group's last quad: its last one
-                    // again, never used), so the wait for a quad's data can
+                    // unconditional (past the group's last quad / oct: its last
+                    // one again, never used), so the wait for a quad's data can
                     // count exactly the loads issued after it
                     const uint32_t nq = min(b * 4 + t + PF, nquads - 1);
                     const int nb = PF == 1 ? ((t + 1) & 1) : PF - 1;
                     qn[nb] = load_quad<2>(qsrc, qvoff, nq * qstride);
-                    an[nb] = load_quad(pap, lane16, nq * 1024u);
+                    if ((t & 1) == 0) {
+                        const uint32_t no = min(b * 2 + (t >> 1) + 1, nocts - 1);
+                        ao[(t >> 1) ^ 1] = load_quad(pap, lane16, no * 1024u);
+                    }
                 }
                 const uint32_t qw[4] = {qcur.x, qcur.y, qcur.z, qcur.w};
-                const uint32_t aw[4] = {acur.x, acur.y, acur.z, acur.w};
+                // this quad's four offsets (16 bits each, in 16-byte units)
+                const uint32_t w0 = (t & 1) ? ao[t >> 1].z : ao[t >> 1].x;
+                const uint32_t w1 = (t & 1) ? ao[t >> 1].w : ao[t >> 1].y;
+                const uint32_t aw[4] = {lo16x16(w0), (w0 >> 16) << 4, lo16x16(w1), (w1 >> 16) << 4};
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int k = t * 4 + u;

@@ -38,6 +38,24 @@ def main(path):
     np.add.at(busy, inv, du)
     print(f"SIMDs seen {len(u)}; last wave end per SIMD: min {last.min():.0f} median {np.median(last):.0f} "
           f"max {last.max():.0f} us")
+    # resident pair waves per CU: the maximum over the launch of waves that
+    # overlap in time on one CU (4 per workgroup: the occupancy the LDS and
+    # registers actually allowed)
+    cu = simd >> 4
+    pr0 = ~is_long
+    ucu, cinv = np.unique(cu[pr0], return_inverse=True)
+    peak = np.zeros(len(ucu), dtype=np.int64)
+    ev_t = np.concatenate([st[pr0], en[pr0]])
+    ev_d = np.concatenate([np.ones(pr0.sum(), np.int64), -np.ones(pr0.sum(), np.int64)])
+    ev_c = np.concatenate([cinv, cinv])
+    o = np.lexsort((ev_d, ev_t))            # ends before starts at equal times
+    cur = np.zeros(len(ucu), dtype=np.int64)
+    for c, d in zip(ev_c[o], ev_d[o]):
+        cur[c] += d
+        if cur[c] > peak[c]:
+            peak[c] = cur[c]
+    vals, cnts = np.unique(peak, return_counts=True)
+    print("peak resident pair waves per CU (waves: CUs):", dict(zip(vals.tolist(), cnts.tolist())))
     # active pair waves over time (1 % bins of the span)
     edges = np.linspace(0, span, 101)
     act = [int(((st < b) & (en > a) & ~is_long).sum()) for a, b in zip(edges[:-1], edges[1:])]
