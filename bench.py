@@ -535,19 +535,23 @@ def timed_steps(S, job, sh, w, steps, warmup, k):
         step()
     if job.native and job.gather_checked is None:
         check_native_gather(S, job, sh.qq, algo, k, w.width)
+    # the timed region holds only the searches (and at N > 1 the gather):
+    # the library's running totals are read once on each side of it
+    st0 = S.stats()
     job.sync()
-    per = {f: [] for f in ("kernel_ms", "wide_ms", "search_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms",
-                           "replay_ms")}
     t_start = time.perf_counter()
     for _ in range(steps):
         res = step()
-        st = S.stats()
-        for f in per:
-            per[f].append(st[f])
     job.sync()
     elapsed = job.max(time.perf_counter() - t_start)
-    return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=S.stats(),
-                              avg={f: float(np.mean(v)) for f, v in per.items()})
+    st = S.stats()
+    n = max(1, st["total_searches"] - st0["total_searches"])
+    avg = {"kernel_ms": (st["total_kernel_ms"] - st0["total_kernel_ms"]) / n,
+           "search_ms": (st["total_search_ms"] - st0["total_search_ms"]) / n}
+    # (host-side breakdown: the last search's)
+    for f in ("wide_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms", "replay_ms"):
+        avg[f] = st[f]
+    return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=st, avg=avg)
 
 
 def fixture_match(w, sh, res, k, world):

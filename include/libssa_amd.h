@@ -63,6 +63,11 @@ typedef struct {
                                 "+"-joined when split over two launches), "" none */
     uint32_t part_retries;   /* searches run again without strip parts because a part's wait for its
                                 group's first part ran into option "part_wait_us" (results unaffected) */
+    /* running totals since the library was loaded (never reset): a caller
+     * times N searches by two reads, with no call between the searches */
+    uint64_t total_searches;
+    double total_kernel_ms;  /* sum of kernel_ms */
+    double total_search_ms;  /* sum of search_ms */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0

@@ -161,6 +161,9 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     S.counters = (bw == BIT_WIDTH_64 || counters_on(cfg())) ? 1 : 0;
     S.replay_ms = t2 - t1;
     S.search_ms = now_ms() - t0;
+    S.total_searches++;
+    S.total_kernel_ms += S.kernel_ms;
+    S.total_search_ms += S.search_ms;
     // m_run's bookkeeping messages (manager.c:147-170)
     const size_t cs = cfg().chunk_size;
     size_t records = 0, entries = 0;
@@ -524,6 +527,9 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         S.kernel_launches = launches;
         S.part_retries = retries;
         S.search_ms = now_ms() - t0;
+        S.total_searches += nq;
+        S.total_kernel_ms += kms;
+        S.total_search_ms += S.search_ms;
         return total;
     }
     for (size_t i = 0; i < nq; i++) {
