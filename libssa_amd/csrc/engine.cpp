@@ -1470,7 +1470,6 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         const int rl32 = rescore32_rl(D, m, A, Q, R, minM, maxM);
         LongArgs ra{};
         if (rl32 > 0) {
-            w.zero_only = 1;                       // wide_kernel only clears the counters
             ra.res = dres;
             ra.groups = D.d_groups;
             ra.lane_len = D.d_lane_len;
@@ -1722,6 +1721,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                         if (D.part_cap < quads * nqf) {
                             dfree(D.d_part);
                             check(hipMalloc((void**)&D.d_part, (size_t)quads * nqf * 4), "strip parts");
+                            check(hipMemsetAsync(D.d_part, 0, (size_t)quads * nqf * 4, st), "memset");
                             D.part_cap = quads * nqf;
                         }
                         if (D.smax_cap < (size_t)D.ngroups * 64 * nqf) {
@@ -1730,7 +1730,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                             D.smax_cap = (size_t)D.ngroups * 64 * nqf;
                         }
                     }
-                    check(hipMemsetAsync(D.d_part, 0, (size_t)quads * nqf * 4, st), "memset");
+                    // this launch's handoff flag value (no per-launch clearing:
+                    // older launches left smaller or different values; never 0,
+                    // the value of fresh memory)
+                    if (++D.part_epoch == 0) ++D.part_epoch;
+                    b.part_epoch = D.part_epoch;
                     b.nparts = parts;
                     b.part_strips = ps;
                     b.nquads = quads;
@@ -1814,8 +1818,17 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
             if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
             check(hipEventRecord(ev_k1, st), "event");
-            check(launch_wide(w, rl32 > 0 ? 64u : wide_threads, st), "wide kernel launch");
-            if (rl32 > 0) check(launch_long(ra, 1, rl32, nw, st), "int32 re-score launch");
+            if (rl32 > 0) {
+                // the int32 tier clears what wide_kernel would have (one launch)
+                LongArgs rz = ra;
+                rz.zero = w.zero;
+                rz.nzero = w.nzero;
+                rz.zero2[0] = w.zero2[0];
+                rz.zero2[1] = w.zero2[1];
+                check(launch_long(rz, 1, rl32, nw, st), "int32 re-score launch");
+            } else {
+                check(launch_wide(w, wide_threads, st), "wide kernel launch");
+            }
             if (want_counts) {
                 // 8/16-bit overflow flags of this view's lanes (counters.hip);
                 // "ordinary" widths are decided from exact values and bounds

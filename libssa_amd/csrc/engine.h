@@ -98,6 +98,7 @@ struct DeviceDB {
     // pair_kernel strip parts (StripArgs::nparts): per quad parts done, per lane running maxima
     uint32_t* d_part = nullptr;
     size_t part_cap = 0;
+    uint32_t part_epoch = 0;              // the last pair launch's handoff flag value (StripArgs::part_epoch)
     uint32_t* d_smax = nullptr;
     size_t smax_cap = 0;
     uint4* d_rowbuf2 = nullptr;           // part 1's row buffer (StripArgs::rowbuf2), as d_rowbuf

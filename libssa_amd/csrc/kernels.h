@@ -71,7 +71,8 @@ struct StripArgs {
     // -- so the SIMDs drain closer together.
     // nparts 1: whole groups, no carry.
     uint32_t nparts, part_strips, nquads;
-    uint32_t* part_done;       // [nquads] parts completed (zeroed per launch)
+    uint32_t* part_done;       // [nquads] part_epoch once the quad's first part is done (never cleared)
+    uint32_t part_epoch;       // this launch's flag value (differs from every earlier launch's)
     uint32_t* part_smax;       // [ngroups * 64]
     uint32_t* part_err;        // set when a wait timed out (the host then runs the search again without parts)
     uint32_t part_wait;        // bound of that wait, s_memrealtime ticks (100 MHz)
@@ -135,6 +136,11 @@ struct LongArgs {
     const uint32_t* list_count;
     int64_t* list_out;
     uint32_t blocks;
+    // (list mode) block 0 clears these as wide_kernel would (WideArgs::zero,
+    // zero2): the tier replaces its launch
+    uint32_t* zero;
+    uint32_t nzero;
+    uint32_t* zero2[2];
 };
 constexpr int kLongWaves = 4;
 
@@ -155,7 +161,6 @@ struct WideArgs {
     uint32_t* zero;            // nzero dwords cleared by block 0 (the next filter pass's counters)
     uint32_t nzero;
     uint32_t* zero2[2];        // and these two dwords (the overflow-flag replay lists' counts), if set
-    uint32_t zero_only;        // 1: only the clearing above (the int32 tier, long_kernel, re-scores the list)
 };
 
 // Device-side top-k candidate filter (single query view, k <= kFilterMaxK).

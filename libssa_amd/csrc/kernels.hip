@@ -384,7 +384,6 @@ strip_f16m_kernel(const StripArgs a) {
 __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
     if (blockIdx.x == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x >= 62 && a.zero2[threadIdx.x - 62]) *a.zero2[threadIdx.x - 62] = 0;
-    if (a.zero_only) return;
     const uint32_t n = min(*a.ovf_count, a.ovf_cap);
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -554,13 +553,23 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
     const int K = (int)a.k;
     const uint32_t per = (a.nblocks + kPrefixWaves - 1) / kPrefixWaves;
     const uint32_t b0 = min(a.nblocks, wave * per), b1 = min(a.nblocks, b0 + per);
+    // (the scan is a chain of merges; its loads run PD blocks ahead so their
+    // latency overlaps it -- a 10 M-entry search has ~150 blocks per wave)
+    constexpr uint32_t PD = 8;
     int32_t run = INT32_MIN;
-    int32_t nxt = b0 < b1 ? a.summary[(size_t)b0 * kFilterMaxK + lane] : INT32_MIN;
-    for (uint32_t b = b0; b < b1; b++) {
-        const int32_t blk = nxt;
-        if (b + 1 < b1) nxt = a.summary[(size_t)(b + 1) * kFilterMaxK + lane];
-        a.before[(size_t)b * kFilterMaxK + lane] = run;
-        run = merge_topk(run, blk, lane, K);
+    int32_t buf[PD];
+#pragma unroll
+    for (uint32_t i = 0; i < PD; i++) buf[i] = b0 + i < b1 ? a.summary[(size_t)(b0 + i) * kFilterMaxK + lane] : INT32_MIN;
+    for (uint32_t b = b0; b < b1; b += PD) {
+#pragma unroll
+        for (uint32_t i = 0; i < PD; i++) {
+            if (b + i < b1) {
+                const int32_t blk = buf[i];
+                if (b + i + PD < b1) buf[i] = a.summary[(size_t)(b + i + PD) * kFilterMaxK + lane];
+                a.before[(size_t)(b + i) * kFilterMaxK + lane] = run;
+                run = merge_topk(run, blk, lane, K);
+            }
+        }
     }
     carry[wave][lane] = run;
     __syncthreads();
@@ -574,12 +583,19 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
     }
     __syncthreads();
     const int32_t c = carry[wave][lane];
-    nxt = b0 < b1 ? a.before[(size_t)b0 * kFilterMaxK + lane] : INT32_MIN;
-    for (uint32_t b = b0; b < b1; b++) {
-        const int32_t st = nxt;
-        if (b + 1 < b1) nxt = a.before[(size_t)(b + 1) * kFilterMaxK + lane];
-        const int32_t t = __builtin_amdgcn_readlane(merge_topk(c, st, lane, K), K - 1);
-        if (lane == 0) a.thresh[b] = t;
+    // (independent per block: every load issued before the merges)
+#pragma unroll
+    for (uint32_t i = 0; i < PD; i++) buf[i] = b0 + i < b1 ? a.before[(size_t)(b0 + i) * kFilterMaxK + lane] : INT32_MIN;
+    for (uint32_t b = b0; b < b1; b += PD) {
+#pragma unroll
+        for (uint32_t i = 0; i < PD; i++) {
+            if (b + i < b1) {
+                const int32_t st = buf[i];
+                if (b + i + PD < b1) buf[i] = a.before[(size_t)(b + i + PD) * kFilterMaxK + lane];
+                const int32_t t = __builtin_amdgcn_readlane(merge_topk(c, st, lane, K), K - 1);
+                if (lane == 0) a.thresh[b + i] = t;
+            }
+        }
     }
 }
 
@@ -798,6 +814,10 @@ __global__ void __launch_bounds__(64 * kLongWaves) long_kernel(const LongArgs a)
     // the re-score tier (LongArgs::list): the workgroup loops over the list,
     // EPW entries at a time (uniform per workgroup: every wave meets the same
     // barriers); otherwise one round, entries seq0 + s of the group order
+    if (a.list && blockIdx.x == 0) {
+        if (threadIdx.x < a.nzero) a.zero[threadIdx.x] = 0;
+        if (threadIdx.x >= 62 && threadIdx.x < 64 && a.zero2[threadIdx.x - 62]) *a.zero2[threadIdx.x - 62] = 0;
+    }
     const uint32_t cnt = a.list ? min(*a.list_count, a.nseq) : a.nseq;
     for (uint32_t bi = blockIdx.x; !a.list || bi * EPW < cnt; bi += a.blocks) {
     const uint32_t s = bi * EPW + wave / W;

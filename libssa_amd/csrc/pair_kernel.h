@@ -157,7 +157,7 @@ pair_kernel(const StripArgs a) {
             if (threadIdx.x == 0) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (__hip_atomic_load(a.part_done + (size_t)wg * nqs + qi, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) < part) {
+                                         __HIP_MEMORY_SCOPE_AGENT) != a.part_epoch) {
                     if (__builtin_amdgcn_s_memrealtime() - t0 >= a.part_wait) {
                         __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -519,7 +519,7 @@ pair_kernel(const StripArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, part + 1, __ATOMIC_RELAXED,
+            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, a.part_epoch, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
