@@ -545,9 +545,13 @@ def timed_steps(S, job, sh, w, steps, warmup, k):
     job.sync()
     elapsed = job.max(time.perf_counter() - t_start)
     st = S.stats()
-    n = max(1, st["total_searches"] - st0["total_searches"])
-    avg = {"kernel_ms": (st["total_kernel_ms"] - st0["total_kernel_ms"]) / n,
-           "search_ms": (st["total_search_ms"] - st0["total_search_ms"]) / n}
+    n = st["total_searches"] - st0["total_searches"]
+    if n > 0:
+        avg = {"kernel_ms": (st["total_kernel_ms"] - st0["total_kernel_ms"]) / n,
+               "search_ms": (st["total_search_ms"] - st0["total_search_ms"]) / n}
+    else:
+        # (a library build without the running totals: SSA_AMD_LIB A/B runs)
+        avg = {"kernel_ms": st["kernel_ms"], "search_ms": st["search_ms"]}
     # (host-side breakdown: the last search's)
     for f in ("wide_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms", "replay_ms"):
         avg[f] = st[f]
