@@ -68,6 +68,8 @@ typedef struct {
     uint64_t total_searches;
     double total_kernel_ms;  /* sum of kernel_ms */
     double total_search_ms;  /* sum of search_ms */
+    uint64_t filter_candidates;  /* scores of the last search the device top-k filter let through to
+                                    the host (every score when it ran without the filter) */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0

@@ -68,7 +68,8 @@ class ssa_amd_stats_t(Structure):
                 ("kernel", ctypes.c_char * 32), ("prep_ms", c_double), ("upload_ms", c_double),
                 ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32),
                 ("long_entries", c_uint32), ("long_kernel", ctypes.c_char * 24), ("part_retries", c_uint32),
-                ("total_searches", c_uint64), ("total_kernel_ms", c_double), ("total_search_ms", c_double)]
+                ("total_searches", c_uint64), ("total_kernel_ms", c_double), ("total_search_ms", c_double),
+                ("filter_candidates", c_uint64)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24

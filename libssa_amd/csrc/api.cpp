@@ -86,11 +86,16 @@ struct SearchResult {
     std::vector<Hit> hits;      // sorted top-k, or the insertion log
 };
 
+// scores the device top-k filter let through to the host (every score of a
+// search that ran without the filter)
+uint64_t candidates(const SearchScores& x) { return x.sparse ? x.cand.size() : (uint64_t)x.entries * x.views; }
+
 void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPlan>& plan) {
     ssa_amd_stats_t& S = stats();
     S.kernel_ms = S.wide_ms = S.d2h_ms = S.prep_ms = S.upload_ms = S.sync_wait_ms = 0;
-    S.cells = S.entries = S.wide_count = S.kernel_bytes = 0;
+    S.cells = S.entries = S.wide_count = S.kernel_bytes = S.filter_candidates = 0;
     for (size_t i = 0; i < sc.size(); i++) {
+        S.filter_candidates += candidates(sc[i]);
         // devices run concurrently: times are the slowest device's
         S.kernel_ms = std::max(S.kernel_ms, sc[i].kernel_ms);
         S.wide_ms = std::max(S.wide_ms, sc[i].wide_ms);
@@ -161,6 +166,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     S.counters = (bw == BIT_WIDTH_64 || counters_on(cfg())) ? 1 : 0;
     S.replay_ms = t2 - t1;
     S.search_ms = now_ms() - t0;
+    if (trace_on()) fprintf(stderr, "trace: run_search to device_search end %.3f, replay %.3f, total %.3f\n", t1 - t0, t2 - t1, S.search_ms);
     S.total_searches++;
     S.total_kernel_ms += S.kernel_ms;
     S.total_search_ms += S.search_ms;
@@ -477,6 +483,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         std::stable_sort(ord.begin(), ord.end(),
                          [&](size_t x, size_t y) { return qviews[x][0].len < qviews[y][0].len; });
         uint32_t launches = 0, retries = 0;
+        uint64_t ncand = 0;
         for (size_t b0 = 0; b0 < nq; b0 += kMaxBatchPipe) {
             const size_t b1 = std::min(nq, b0 + kMaxBatchPipe);
             std::vector<QueryView> vs;
@@ -489,6 +496,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
                 kms += stats().kernel_ms;
                 cells += stats().cells;
                 retries += stats().part_retries;
+                ncand += stats().filter_candidates;
                 launches++;
                 const size_t n = std::min(hitcount, R.hits.size());
                 for (size_t j = 0; j < n; j++) {
@@ -509,6 +517,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
                 const size_t i = ord[bi];
                 const SearchScores& x = sc[bi - b0];
                 cells += x.cells;
+                ncand += candidates(x);
                 TopK heap(hitcount);
                 replay(x, D.meta, qviews[i], heap, nullptr);
                 const std::vector<Hit> hits = heap.sorted();
@@ -526,6 +535,7 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         S.cells = cells;
         S.kernel_launches = launches;
         S.part_retries = retries;
+        S.filter_candidates = ncand;
         S.search_ms = now_ms() - t0;
         S.total_searches += nq;
         S.total_kernel_ms += kms;

@@ -1933,6 +1933,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.ovf_stride = 0;
                 f.nviews = 1;
                 f.counters = reg;
+                f.status = gate + 2;
                 f.cand = (uint2*)(reg + kFilterHeader);
                 check(launch_filter(f, st), "filter launch");
                 check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
@@ -1962,6 +1963,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             f.ovf_stride = 0;
             f.nviews = 1;
             f.counters = (uint32_t*)D.d_fbuf;
+            f.status = gate + 2;
             f.cand = (uint2*)(f.counters + kFilterHeader);
             f.nq = (uint32_t)V;
             f.q_scores = E;
@@ -1992,6 +1994,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             f.ovf_stride = (uint32_t)(ovf_capv + 1);
             f.nviews = (uint32_t)(multi ? V : 1);
             f.counters = D.d_fbuf;
+            f.status = gate + 2;
             f.cand = (uint2*)(D.d_fbuf + kFilterHeader);
             check(launch_filter(f, st), "filter launch");
             // one copy: counters (incl. the overflow counts) + the first candidates
@@ -2005,8 +2008,12 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * (pre + 1), hipMemcpyDeviceToHost, st), "D2H overflow");
             check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * pre, hipMemcpyDeviceToHost, st), "D2H wide");
         }
+        // the strip-part wait status: the filter passes copy it into their
+        // candidate headers (word 2); only a search without them reads it back
         uint32_t* const h_perr = (uint32_t*)(D.h_cnt + 2 * kMaxBatchPipe) + 2;
-        if (parts_used) check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
+        const bool perr_in_header = ind || out.sparse;
+        if (parts_used && !perr_in_header)
+            check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
         check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
         check(hipStreamSynchronize(st), "search");
@@ -2014,7 +2021,15 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // a strip part gave up waiting for its group's first part: this
         // launch's scores are incomplete -- the caller runs the search again
         // without parts (never fatal: a slow predecessor is a timing event)
-        if (parts_used && *h_perr) return false;
+        if (parts_used) {
+            uint32_t perr = 0;
+            if (ind) {
+                for (size_t vv = 0; vv < V; vv++) perr |= ((const uint32_t*)((const uint8_t*)D.h_fbuf + vv * hreg))[2];
+            } else {
+                perr = out.sparse ? D.h_fbuf[2] : *h_perr;
+            }
+            if (perr) return false;
+        }
         const double t_post0 = now_ms();
 
         {
@@ -2022,6 +2037,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             check(hipEventElapsedTime(&u, D.ev[4], ev_k0), "elapsed");
             upload += u;
         }
+        if (trace_on()) fprintf(stderr, "trace: sync-wait %.3f\n", now_ms() - t_sync0);
         // exact int64 scores of overflowed lanes: view vv's list and scores
         auto take_wide = [&](size_t vv, uint32_t nov, SearchScores& dst, size_t key_view) {
             const uint32_t* ov = D.d_ovf + (piped ? vv * (ovf_capv + 1) : 0);
@@ -2091,14 +2107,15 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 cand = more.data();
             }
             // candidates by insertion position; out.cand holds view * E + entry
-            std::vector<uint2> cs(cand, cand + nc);
-            std::sort(cs.begin(), cs.end(), [](const uint2& x, const uint2& y) { return x.x < y.x; });
+            // (the scores land first, then the bare positions are sorted)
             out.cand.resize(nc);
             for (uint32_t i = 0; i < nc; i++) {
-                const uint32_t x = multi ? D.h_order[cs[i].x] : cs[i].x;
-                out.cand[i] = x;
-                D.h_scores[x] = (int32_t)cs[i].y;
+                out.cand[i] = cand[i].x;
+                D.h_scores[multi ? D.h_order[cand[i].x] : cand[i].x] = (int32_t)cand[i].y;
             }
+            std::sort(out.cand.begin(), out.cand.end());
+            if (multi)
+                for (uint32_t i = 0; i < nc; i++) out.cand[i] = D.h_order[out.cand[i]];
             for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
                 const uint32_t nov = D.h_fbuf[3 + vv];
                 if (nov) take_wide(multi ? vv : v, nov, out, multi ? vv : v);
@@ -2106,6 +2123,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         } else {
             take_wide(v, D.h_ovf[0], out, v);
         }
+        if (trace_on()) fprintf(stderr, "trace: candidates %.3f (%zu)\n", now_ms() - t_post0, out.cand.size());
         float t;
         if (fused) {
             // one launch for all views: from that launch to the join of the DP

@@ -183,8 +183,10 @@ struct FilterArgs {
     int32_t* before;           // [nblocks][kFilterMaxK] scan scratch
     const uint32_t* ovf_count; // view v's count at ovf_count[v * ovf_stride], copied into counters[3 + v]
     uint32_t ovf_stride, nviews;
-    uint32_t* counters;        // [0] candidates, [3 + v] overflowed lanes of view v
+    uint32_t* counters;        // [0] candidates, [2] *status, [3 + v] overflowed lanes of view v
                                // (one host copy fetches everything)
+    const uint32_t* status;    // the pair launch's strip-part wait status word (copied into
+                               // counters[2]: no separate read-back); null: none
     uint2* cand;               // [n] (insertion position, score) of the candidates, unordered;
                                // at counters + kFilterHeader
     // several independent queries in one pass (a fused batch): blockIdx.y =

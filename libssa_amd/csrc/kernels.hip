@@ -467,9 +467,41 @@ __global__ void __launch_bounds__(64) wide_kernel(const WideArgs a) {
 // (INT32_MIN while fewer than k).  Overflowed entries are left out of the
 // maxima (that only lowers the bounds) and always forwarded.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int32_t wave_max(int32_t x) {
-    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
+// x of lane (lane ^ J), J a power of two below 64, without the LDS
+// crossbar (a ds_bpermute costs an LDS round trip per step of the filter's
+// dependent merge chains): DPP within rows of 16 -- quad_perm for 1 and 2,
+// row_half_mirror then a quad reversal for 4, row_ror:8 for 8 -- and
+// gfx950's v_permlane16_swap / v_permlane32_swap across rows.  The swaps
+// exchange the odd rows (upper half) of their first operand with the even
+// rows (lower half) of their second; with x in both, the first result holds
+// the even rows' (lower half's) values in every row pair (half), the second
+// the odd rows' (upper half's).
+template <int J>
+__device__ __forceinline__ int32_t lane_xor(int32_t x, int lane) {
+    static_assert(J == 1 || J == 2 || J == 4 || J == 8 || J == 16 || J == 32, "lane_xor<J>");
+    if constexpr (J == 1) return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    if constexpr (J == 2) return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    if constexpr (J == 4)                                                             // 7 - i, then 3 - i
+        return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false), 0x1B, 0xf, 0xf, false);
+    if constexpr (J == 8) return __builtin_amdgcn_mov_dpp(x, 0x128, 0xf, 0xf, false);  // row_ror:8
+    if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)x, false, false);
+        return (int32_t)((lane & 16) ? r[0] : r[1]);
+    }
+    if constexpr (J == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)x, false, false);
+        return (int32_t)((lane & 32) ? r[0] : r[1]);
+    }
     return x;
+}
+
+__device__ __forceinline__ int32_t wave_max(int32_t x, int lane) {
+    x = max(x, lane_xor<1>(x, lane));
+    x = max(x, lane_xor<2>(x, lane));
+    x = max(x, lane_xor<4>(x, lane));
+    x = max(x, lane_xor<8>(x, lane));
+    x = max(x, lane_xor<16>(x, lane));
+    return max(x, lane_xor<32>(x, lane));
 }
 
 // Inserts x into a descending list held one element per lane (lanes < K),
@@ -506,12 +538,17 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a0) {
     __shared__ int32_t mini_max[kMinisPerBlock];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * kFilterBlock;
-    for (int i = 0; i < kMinisPerBlock / 4; i++) {
-        const int m = i * 4 + wave;                 // this wave's mini: 64 consecutive entries
-        const uint32_t e = base + m * kMini + lane;
-        const int32_t x = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
-        const int32_t mx = wave_max(x);
-        if (lane == 0) mini_max[m] = mx;
+    constexpr int MW = kMinisPerBlock / 4;          // minis per wave, every load issued first
+    int32_t x[MW];
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        const uint32_t e = base + (i * 4 + wave) * kMini + lane;   // mini i*4+wave: 64 consecutive entries
+        x[i] = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
+    }
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        const int32_t mx = wave_max(x[i], lane);
+        if (lane == 0) mini_max[i * 4 + wave] = mx;
     }
     __syncthreads();
     if (wave == 0) {
@@ -531,19 +568,29 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a0) {
 // Top-k of two descending lists (one element per lane, lanes >= K hold
 // INT32_MIN): max(a[i], b[63-i]) holds the 64 largest of the union as a
 // bitonic sequence; six compare-exchange stages sort it.
+// (y of lane 63 - lane = lane ^ 63: row_mirror, then the row pairs and halves
+// swapped; every step a VALU lane move, see lane_xor)
+template <int J>
+__device__ __forceinline__ int32_t bitonic_step(int32_t v, int lane) {
+    const int32_t o = lane_xor<J>(v, lane);
+    return (lane & J) ? min(v, o) : max(v, o);
+}
 __device__ __forceinline__ int32_t merge_topk(int32_t x, int32_t y, int lane, int K) {
-    int32_t v = max(x, __shfl(y, 63 - lane));
-    for (int j = 32; j > 0; j >>= 1) {
-        const int32_t o = __shfl_xor(v, j);
-        v = (lane & j) ? min(v, o) : max(v, o);
-    }
+    const int32_t yr = lane_xor<32>(lane_xor<16>(__builtin_amdgcn_mov_dpp(y, 0x140, 0xf, 0xf, false), lane), lane);
+    int32_t v = max(x, yr);
+    v = bitonic_step<32>(v, lane);
+    v = bitonic_step<16>(v, lane);
+    v = bitonic_step<8>(v, lane);
+    v = bitonic_step<4>(v, lane);
+    v = bitonic_step<2>(v, lane);
+    v = bitonic_step<1>(v, lane);
     return lane < K ? v : INT32_MIN;
 }
 
 // Exclusive prefix of the block summaries under top-k merge, as a blocked
 // scan: each of 16 waves scans its run of blocks (keeping the state before
-// every block), wave 0 scans the 16 run totals, and every wave merges its
-// carry-in into the stored states.  T[b] = k-th largest of all mini maxima
+// every block), the 16 run totals are scanned across the waves, and every
+// wave merges its carry-in into the stored states.  T[b] = k-th largest of all mini maxima
 // of blocks < b.
 constexpr int kPrefixWaves = 16;
 __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterArgs a0) {
@@ -571,18 +618,21 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
             }
         }
     }
-    carry[wave][lane] = run;
+    // the waves' carries: an inclusive scan of the run totals in log2(16)
+    // merge steps (Kogge-Stone over the waves; the top-k merge is associative
+    // and commutative), then shifted by one wave
+    int32_t acc = run;
+    carry[wave][lane] = acc;
     __syncthreads();
-    if (wave == 0) {
-        int32_t c = INT32_MIN;
-        for (int w = 0; w < kPrefixWaves; w++) {
-            const int32_t t = carry[w][lane];
-            carry[w][lane] = c;
-            c = merge_topk(c, t, lane, K);
-        }
+#pragma unroll
+    for (int d = 1; d < kPrefixWaves; d <<= 1) {
+        const int32_t o = wave >= d ? carry[wave - d][lane] : INT32_MIN;
+        __syncthreads();
+        acc = merge_topk(acc, o, lane, K);
+        carry[wave][lane] = acc;
+        __syncthreads();
     }
-    __syncthreads();
-    const int32_t c = carry[wave][lane];
+    const int32_t c = wave > 0 ? carry[wave - 1][lane] : INT32_MIN;
     // (independent per block: every load issued before the merges)
 #pragma unroll
     for (uint32_t i = 0; i < PD; i++) buf[i] = b0 + i < b1 ? a.before[(size_t)(b0 + i) * kFilterMaxK + lane] : INT32_MIN;
@@ -603,6 +653,7 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     const FilterArgs a = filter_query(a0);
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     if (e < a.nviews) a.counters[3 + e] = a.ovf_count[(size_t)e * a.ovf_stride];
+    if (e == 0 && a.status) a.counters[2] = *a.status;
     if (e >= a.n) return;
     const int32_t x = a.scores[a.order ? a.order[e] : e];
     const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);

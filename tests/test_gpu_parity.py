@@ -975,6 +975,66 @@ def test_device_topk_filter_matches_full_scan(pattern):
         S.free_sequence(qq)
 
 
+def _filter_candidates(sc, k):
+    """numpy restatement of the device filter's bound (kernels.hip, above
+    filter_block): entry e of mini m (64 entries) of block b (4096) is
+    forwarded iff its score beats both the k-th largest maximum of the
+    earlier minis of b and the k-th largest maximum of all minis of the
+    blocks before b (INT32_MIN while fewer than k)."""
+    lo = np.iinfo(np.int32).min
+    n = len(sc)
+    nm, nb = -(-n // 64), -(-n // 4096)
+    pad = np.full(nb * 4096, lo, np.int64)
+    pad[:n] = sc
+    mm = pad.reshape(nb * 64, 64).max(1).reshape(nb, 64)
+
+    def kth(v):
+        return lo if len(v) < k else int(np.sort(v)[::-1][k - 1])
+    t_block = np.array([kth(mm[:b].ravel()) for b in range(nb)], np.int64)
+    t_local = np.array([[kth(mm[b, :m]) for m in range(64)] for b in range(nb)], np.int64).ravel()[:nm]
+    e = np.arange(n)
+    return int(np.count_nonzero(sc > np.maximum(t_block[e // 4096], t_local[e // 64])))
+
+
+@pytest.mark.parametrize("n,pattern", [(90000, "random"), (90000, "rising"), (700000, "random"),
+                                       (700000, "falling")])
+def test_device_filter_candidate_count_is_exact(n, pattern):
+    """The filter's lane moves (DPP, v_permlane16/32_swap) and its
+    cross-wave scan of the block summaries must give exactly the bounds the
+    definition gives: stats filter_candidates equals the count of the numpy
+    restatement on the oracle's scores (700 k entries: 171 blocks, all 16
+    scan waves busy), and the top-k equals the oracle's."""
+    rng = np.random.default_rng(n + len(pattern))
+    q = syn.protein_query(24, 5)
+    lens = rng.integers(4, 20, n)
+    if pattern == "rising":          # scores climb with the ID: most entries forwarded
+        seqs = [np.concatenate([q[: 1 + (i * 23) // n], rng.choice(syn.AA_CODES, 3)]) for i in range(n)]
+    elif pattern == "falling":       # best entries first: the bounds rise early
+        seqs = [np.concatenate([q[: 1 + ((n - 1 - i) * 23) // n], rng.choice(syn.AA_CODES, 3)]) for i in range(n)]
+    else:
+        seqs = None
+    if seqs is None:
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        codes = rng.choice(syn.AA_CODES, int(off[-1])).astype(np.uint8)
+    else:
+        codes = np.concatenate(seqs).astype(np.uint8)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum([len(s) for s in seqs], out=off[1:])
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    exp = po.scores(S.SW, q, codes, off, M, -11, -1)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        ids = np.arange(n, dtype=np.uint64)
+        for k in (1, 10, 64):
+            got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+            assert got == po.topk(exp, ids, k), (pattern, k)
+            assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k)
+        S.free_sequence(qq)
+
+
 @pytest.mark.parametrize("mode", ["both_strands", "trans_query"])
 def test_multiview_device_filter_matches_full_scan(mode):
     """Multi-view searches (NUCLEOTIDE both strands: 2 query views;
