@@ -13,6 +13,7 @@
 #include <numeric>
 #include <thread>
 
+#include "bulk_alloc.h"
 #include "engine.h"
 
 namespace ssa {
@@ -149,7 +150,7 @@ namespace {
 struct Staged {
     EntryMeta meta;
     std::vector<uint64_t> off;       // entry -> offset into codes
-    std::vector<uint8_t> codes;
+    Bytes codes;
     std::vector<std::pair<size_t, size_t>> unknown;   // (record, count) with unknown symbols
 };
 
@@ -215,36 +216,40 @@ void stage_range(size_t r0, size_t r1, Staged& S) {
 
 unsigned host_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
 
+// The parse threads' parts, merged by reference: one metadata array over all
+// entries, and per entry a pointer to its codes inside its part (the parts'
+// code buffers are never concatenated: 3.6 GB for the 10 M DB).
+struct StagedDB {
+    EntryMeta meta;
+    std::vector<const uint8_t*> src;
+    std::vector<Staged> parts;
+};
+
 // The plugin is called from several threads at once, as the reference's
 // own search threads do (adp_next_chunk runs in every worker).
-void stage_from_plugin(Staged& S, size_t rb, size_t re) {
+void stage_from_plugin(StagedDB& S, size_t rb, size_t re) {
     const size_t count = re - rb;
     const unsigned nth = count < 20000 ? 1u : host_threads();
-    std::vector<Staged> part(nth);
+    S.parts.assign(nth, Staged());
     std::vector<std::thread> pool;
     for (unsigned t = 0; t < nth; t++)
-        pool.emplace_back([&, t]() { stage_range(rb + count * t / nth, rb + count * (t + 1) / nth, part[t]); });
+        pool.emplace_back([&, t]() { stage_range(rb + count * t / nth, rb + count * (t + 1) / nth, S.parts[t]); });
     for (auto& th : pool) th.join();
     S.meta.records = count;
-    size_t ne = 0, nc = 0;
-    for (auto& P : part) {
-        ne += P.meta.size();
-        nc += P.codes.size();
-    }
+    size_t ne = 0;
+    for (auto& P : S.parts) ne += P.meta.size();
     S.meta.id.reserve(ne); S.meta.strand.reserve(ne); S.meta.frame.reserve(ne); S.meta.len.reserve(ne);
-    S.off.reserve(ne);
-    S.codes.reserve(nc);
-    for (auto& P : part) {
-        const uint64_t base = S.codes.size();
+    S.src.reserve(ne);
+    for (auto& P : S.parts) {
         S.meta.id.insert(S.meta.id.end(), P.meta.id.begin(), P.meta.id.end());
         S.meta.strand.insert(S.meta.strand.end(), P.meta.strand.begin(), P.meta.strand.end());
         S.meta.frame.insert(S.meta.frame.end(), P.meta.frame.begin(), P.meta.frame.end());
         S.meta.len.insert(S.meta.len.end(), P.meta.len.begin(), P.meta.len.end());
-        for (uint64_t o : P.off) S.off.push_back(o + base);
-        S.codes.insert(S.codes.end(), P.codes.begin(), P.codes.end());
+        for (uint64_t o : P.off) S.src.push_back(P.codes.data() + o);
         S.meta.residues += P.meta.residues;
         for (auto& u : P.unknown) print_warning("%ld unknown symbols found and set to zero", (long)u.second);
-        P = Staged();
+        P.meta = EntryMeta();
+        P.off = std::vector<uint64_t>();
     }
 }
 
@@ -253,15 +258,17 @@ struct HostPack {
     EntryMeta meta;
     std::vector<GroupDesc> groups;
     std::vector<uint32_t> lane_len, lane_out;
-    std::vector<uint8_t> res;           // blocks * 1 KiB
+    Bytes res;                          // blocks * 1 KiB
     std::vector<uint8_t> code_of;
     uint64_t blocks = 0;
 };
 
 void build_host_pack(HostPack& H, size_t rb, size_t re) {
-    Staged S;
+    const double t0 = now_ms();
+    StagedDB S;
     stage_from_plugin(S, rb, re);
     const size_t E = S.meta.size();
+    const double t1 = now_ms();
 
     // length-sorted groups of 64 lanes (longest first: long waves start
     // early); a stable counting sort by length, entry order within a length
@@ -292,19 +299,18 @@ void build_host_pack(HostPack& H, size_t rb, size_t re) {
     }
     if (blocks >= (1ull << 32)) fatal("DB shard too large for one device (%llu KiB of residues)", (unsigned long long)blocks);
     H.blocks = blocks;
+    const double t2 = now_ms();
     const unsigned nth = host_threads();
     // compact alphabet: the residue codes that occur, in code order; the
     // padding column gets the next code.  Pair-symbol profiles scale with
     // (alpha+1)^2, so a 20-letter DB uses 441 rows instead of 1024.
-    std::vector<std::array<uint8_t, 256>> seen(nth);
+    std::vector<std::array<uint8_t, 256>> seen(S.parts.size());
     {
         std::vector<std::thread> pool;
-        const size_t nc = S.codes.size();
-        for (unsigned t = 0; t < nth; t++)
+        for (size_t t = 0; t < S.parts.size(); t++)
             pool.emplace_back([&, t]() {
                 seen[t].fill(0);
-                const uint8_t* c = S.codes.data();
-                for (size_t i = nc * t / nth, e = nc * (t + 1) / nth; i < e; i++) seen[t][c[i]] = 1;
+                for (const uint8_t c : S.parts[t].codes) seen[t][c] = 1;
             });
         for (auto& th : pool) th.join();
     }
@@ -322,12 +328,16 @@ void build_host_pack(HostPack& H, size_t rb, size_t re) {
     const uint8_t pad = (uint8_t)H.code_of.size();
     H.lane_len.assign((size_t)ngroups * 64, 0);
     H.lane_out.assign((size_t)ngroups * 64, 0xffffffffu);
-    H.res.assign((size_t)blocks * 1024, pad);
+    const double t3 = now_ms();
+    // (no serial fill: every group's thread pads its own blocks)
+    H.res.resize((size_t)blocks * 1024);
+    const double t4 = now_ms();
     std::vector<std::thread> pool;
     for (unsigned t = 0; t < nth; t++) {
         pool.emplace_back([&, t]() {
             for (uint32_t g = t; g < ngroups; g += nth) {
                 uint8_t* gbase = H.res.data() + (size_t)H.groups[g].blk * 1024;
+                memset(gbase, pad, (size_t)(H.groups[g].ncols + 15) / 16 * 1024);
                 for (uint32_t l = 0; l < 64; l++) {
                     const size_t pos = (size_t)g * 64 + l;
                     if (pos >= E) break;
@@ -335,7 +345,7 @@ void build_host_pack(HostPack& H, size_t rb, size_t re) {
                     const uint32_t n = S.meta.len[e];
                     H.lane_len[pos] = n;
                     H.lane_out[pos] = e;
-                    const uint8_t* src = S.codes.data() + S.off[e];
+                    const uint8_t* src = S.src[e];
                     for (uint32_t c = 0; c < n; c++) gbase[(size_t)(c / 16) * 1024 + l * 16 + (c & 15)] = remap[src[c]];
                 }
             }
@@ -343,10 +353,14 @@ void build_host_pack(HostPack& H, size_t rb, size_t re) {
     }
     for (auto& th : pool) th.join();
     H.meta = std::move(S.meta);
+    if (trace_on())
+        fprintf(stderr, "trace: pack stage %.1f ms, sort %.1f, alphabet %.1f, fill %.1f, scatter %.1f ms\n", t1 - t0,
+                t2 - t1, t3 - t2, t4 - t3, now_ms() - t4);
 }
 
 void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     const Config& C = cfg();
+    const double t_al0 = now_ms();
     D.release();
     check(hipSetDevice(dev), "hipSetDevice");
     D.device = dev;
@@ -393,6 +407,8 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     // overflow counters, then the long-entry dispatch gate (TableArgs::gate)
     dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe + 16, "overflow counters");
     check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe + 16, hipHostMallocDefault), "pinned");
+    const double t_up0 = now_ms();
+    if (trace_on()) fprintf(stderr, "trace: pack device allocations %.1f ms\n", t_up0 - t_al0);
     D.upblk_cap = kUpHeader + 16384 + 4096;
     dalloc((void**)&D.d_upblk, D.upblk_cap, "per-search uploads");
     D.d_matrix = (int64_t*)D.d_upblk;
@@ -416,6 +432,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         dalloc((void**)&D.d_entry_lane, el.size() * 4, "entry lanes");
         check(hipMemcpy(D.d_entry_lane, el.data(), el.size() * 4, hipMemcpyHostToDevice), "H2D");
     }
+    if (trace_on()) fprintf(stderr, "trace: pack upload %.1f ms (%zu B residues)\n", now_ms() - t_up0, H.res.size());
     D.ngroups = (uint32_t)H.groups.size();
     D.group_ncols.resize(H.groups.size());
     D.ncols_sum = 0;
@@ -424,8 +441,9 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         D.ncols_sum += H.groups[g].ncols;
     }
     D.nblocks = H.blocks;
-    D.len_sorted = H.meta.len;
-    std::sort(D.len_sorted.begin(), D.len_sorted.end());
+    // ascending lengths: the lanes hold the entries longest first (padding
+    // lanes of the last group at the end, length 0), so reversed
+    D.len_sorted.assign(H.lane_len.rbegin() + (H.lane_len.size() - E), H.lane_len.rend());
     D.meta = std::move(H.meta);
     D.lane_out = std::move(H.lane_out);
     D.code_of = std::move(H.code_of);
@@ -495,9 +513,14 @@ bool ensure_device_db(size_t slot, const SlotPlan& p) {
         D.strands == C.strands && D.dgencode == C.d_gencode && D.rec_begin == p.rec_begin && D.rec_end == p.rec_end)
         return false;
     check(hipSetDevice(p.device), "hipSetDevice");
-    HostPack H;
-    build_host_pack(H, p.rec_begin, p.rec_end);
-    upload_pack(D, H, p.device);
+    const double t0 = now_ms();
+    {
+        HostPack H;
+        build_host_pack(H, p.rec_begin, p.rec_end);
+        upload_pack(D, H, p.device);
+        if (trace_on()) fprintf(stderr, "trace: pack build+upload %.1f ms\n", now_ms() - t0);
+    }
+    if (trace_on()) fprintf(stderr, "trace: pack incl. host frees %.1f ms\n", now_ms() - t0);
     D.rec_begin = p.rec_begin;
     D.rec_end = p.rec_end;
     return true;

@@ -24,11 +24,12 @@
 #include <thread>
 #include <vector>
 
+#include "bulk_alloc.h"
 #include "libssa_extern_db.h"
 
 namespace {
 struct FastaDB {
-    std::vector<char> arena;
+    ssa::Chars arena;                   // (no zeroing resize, huge pages: bulk_alloc.h)
     std::vector<seqinfo_t> recs;
 };
 FastaDB* g_db = nullptr;
@@ -40,7 +41,7 @@ inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c ==
 // header is ignored.  `first_in_record` is set when the piece starts inside
 // a record (never: pieces are cut at record starts, except piece 0).
 struct Piece {
-    std::vector<char> res;
+    ssa::Chars res;
     std::vector<size_t> offs;   // record starts in res
 };
 
@@ -53,6 +54,7 @@ void parse_piece(const char* p, const char* end, bool at_line_start, Piece& out)
             out.offs.push_back(out.res.size());
             in_rec = true;
         } else if (in_rec) {
+            // (uninitialised growth: the line's bytes are written right here)
             const size_t base = out.res.size();
             out.res.resize(base + (size_t)(le - p));
             char* w = out.res.data() + base;
