@@ -151,6 +151,7 @@ struct Staged {
     EntryMeta meta;
     std::vector<uint64_t> off;       // entry -> offset into codes
     Bytes codes;
+    std::array<uint8_t, 256> seen{};     // codes that occur
     std::vector<std::pair<size_t, size_t>> unknown;   // (record, count) with unknown symbols
 };
 
@@ -164,6 +165,7 @@ void stage_range(size_t r0, size_t r1, Staged& S) {
         if (!si) break;
         if (si->seqlen == 0) continue;
         const size_t n = si->seqlen;
+        const size_t cb = S.codes.size();
         auto add = [&](const uint8_t* c, size_t len, int strand, int frame) {
             M.id.push_back(id);
             M.strand.push_back((uint8_t)strand);
@@ -211,6 +213,10 @@ void stage_range(size_t r0, size_t r1, Staged& S) {
             M.residues += n;
         }
         if (unknown > 0) S.unknown.push_back({id, unknown});
+        // the codes that occur (the compact alphabet), marked while the
+        // record's codes are still in cache
+        const uint8_t* cw = S.codes.data();
+        for (size_t i = cb, e = S.codes.size(); i < e; i++) S.seen[cw[i]] = 1;
     }
 }
 
@@ -236,16 +242,25 @@ void stage_from_plugin(StagedDB& S, size_t rb, size_t re) {
         pool.emplace_back([&, t]() { stage_range(rb + count * t / nth, rb + count * (t + 1) / nth, S.parts[t]); });
     for (auto& th : pool) th.join();
     S.meta.records = count;
-    size_t ne = 0;
-    for (auto& P : S.parts) ne += P.meta.size();
-    S.meta.id.reserve(ne); S.meta.strand.reserve(ne); S.meta.frame.reserve(ne); S.meta.len.reserve(ne);
-    S.src.reserve(ne);
+    // the parts' entries at their prefix offsets, one thread per part
+    std::vector<size_t> at(nth + 1, 0);
+    for (unsigned t = 0; t < nth; t++) at[t + 1] = at[t] + S.parts[t].meta.size();
+    const size_t ne = at[nth];
+    S.meta.id.resize(ne); S.meta.strand.resize(ne); S.meta.frame.resize(ne); S.meta.len.resize(ne);
+    S.src.resize(ne);
+    pool.clear();
+    for (unsigned t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() {
+            Staged& P = S.parts[t];
+            const size_t b = at[t], n = P.meta.size();
+            std::copy(P.meta.id.begin(), P.meta.id.end(), S.meta.id.begin() + b);
+            std::copy(P.meta.strand.begin(), P.meta.strand.end(), S.meta.strand.begin() + b);
+            std::copy(P.meta.frame.begin(), P.meta.frame.end(), S.meta.frame.begin() + b);
+            std::copy(P.meta.len.begin(), P.meta.len.end(), S.meta.len.begin() + b);
+            for (size_t i = 0; i < n; i++) S.src[b + i] = P.codes.data() + P.off[i];
+        });
+    for (auto& th : pool) th.join();
     for (auto& P : S.parts) {
-        S.meta.id.insert(S.meta.id.end(), P.meta.id.begin(), P.meta.id.end());
-        S.meta.strand.insert(S.meta.strand.end(), P.meta.strand.begin(), P.meta.strand.end());
-        S.meta.frame.insert(S.meta.frame.end(), P.meta.frame.begin(), P.meta.frame.end());
-        S.meta.len.insert(S.meta.len.end(), P.meta.len.begin(), P.meta.len.end());
-        for (uint64_t o : P.off) S.src.push_back(P.codes.data() + o);
         S.meta.residues += P.meta.residues;
         for (auto& u : P.unknown) print_warning("%ld unknown symbols found and set to zero", (long)u.second);
         P.meta = EntryMeta();
@@ -304,21 +319,11 @@ void build_host_pack(HostPack& H, size_t rb, size_t re) {
     // compact alphabet: the residue codes that occur, in code order; the
     // padding column gets the next code.  Pair-symbol profiles scale with
     // (alpha+1)^2, so a 20-letter DB uses 441 rows instead of 1024.
-    std::vector<std::array<uint8_t, 256>> seen(S.parts.size());
-    {
-        std::vector<std::thread> pool;
-        for (size_t t = 0; t < S.parts.size(); t++)
-            pool.emplace_back([&, t]() {
-                seen[t].fill(0);
-                for (const uint8_t c : S.parts[t].codes) seen[t][c] = 1;
-            });
-        for (auto& th : pool) th.join();
-    }
     uint8_t remap[256] = {0};
     H.code_of.clear();
     for (int c = 0; c < 256; c++) {
         bool any = false;
-        for (auto& v : seen) any |= v[c] != 0;
+        for (auto& P : S.parts) any |= P.seen[c] != 0;
         if (any) {
             remap[c] = (uint8_t)H.code_of.size();
             H.code_of.push_back((uint8_t)c);
