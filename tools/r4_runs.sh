@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments, one function per run (the command lines the round-4
 # profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
-#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
+#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
 set -o pipefail
 
 r4_ab() (
@@ -279,6 +279,20 @@ r4_tl_jag() (
       python tools/timeline.py gpurun_out/r4/tljag/p$p.npy > gpurun_out/r4/tljag/p$p.txt || exit 1
       python -c "import json; d=json.loads(open('gpurun_out/r4/tljag/p$p.json').read().strip().splitlines()[-1]); print('p$p', d['kernel']['kernel_gcups'])"
       grep -E "span|per SIMD" gpurun_out/r4/tljag/p$p.txt
+    done
+)
+
+r4_np_sweep() (
+    # pair-kernel strip height (bench --pair-np) on C2, C3 and the DNA C5 share
+    mkdir -p gpurun_out/r4/np
+    run() {  # name, args
+      local n=$1; shift
+      timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-north-star --no-cpu-baseline "$@" > gpurun_out/r4/np/$n.json 2> gpurun_out/r4/np/$n.err || { tail -20 gpurun_out/r4/np/$n.err; return 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/r4/np/$n.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['kernel']['kernel_gcups'], d['kernel']['avg_ms'], d['config'].get('pair_strip_rows'), d.get('topk_vs_reference'))"
+    }
+    for np_ in ${NPS:-0 24 32 36 40}; do
+      run c5s_np$np_ --config c5 --seqs 1000000 --steps 3 --pair-np $np_ || exit 1
+      run c2_np$np_ --config c2 --pair-np $np_ || exit 1
     done
 )
 
