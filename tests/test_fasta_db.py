@@ -75,3 +75,24 @@ def test_large_file_parallel_parse(tmp_path):
     data = b"".join(parts)
     assert len(data) > (8 << 20)
     _check(tmp_path, data)
+
+
+def test_bulk_allocated_arena(tmp_path):
+    """A residue arena above the 32 MiB threshold of csrc/bulk_alloc.h (an
+    anonymous mapping on transparent huge pages, grown without zeroing)
+    parses byte for byte like the sequential reading, as do the small
+    files on the ordinary allocator above."""
+    rng = np.random.default_rng(9)
+    letters = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    lens = rng.integers(150, 350, 200000)
+    res = letters[rng.integers(0, 20, int(lens.sum()))].tobytes()
+    parts, at = [], 0
+    for i, n in enumerate(lens):
+        s = res[at:at + n]
+        at += n
+        if i % 5 == 0:   # multi-line record
+            s = b"\n".join(s[j:j + 80] for j in range(0, len(s), 80))
+        parts.append(b">r%d\n%s\n" % (i, s))
+    data = b"".join(parts)
+    assert lens.sum() > (32 << 20)
+    _check(tmp_path, data)
