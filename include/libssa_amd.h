@@ -111,10 +111,10 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)
  *   "pair_ticket" 1|0    pair-kernel workgroups take the next groups in start order
  *                        (an atomic ticket; default) or in blockIdx order
- *   "pair_parts" 0|1|2   pair-kernel groups run as 2 dependent work units of consecutive
- *                        strips (all groups' first parts, then all second parts),
- *                        so the launch ends on small units: 0 (default) for groups of
- *                        at least 4 strips, 1 never, 2 always
+ *   "pair_parts" 0|1|2|3 pair-kernel groups run as 2 (or 3) dependent work units of
+ *                        consecutive strips (all groups' first parts, then all second
+ *                        parts, ...), so the launch ends on small units: 0 (default) 2
+ *                        for groups of at least 4 strips, 1 never, 2 always, 3 three
  *   "rescore32" 1|0      entries the DP kernels cannot score exactly (overflow) are re-scored
  *                        by the int32 long-entry kernel, one wave per entry, whenever int32 is
  *                        exact for the DB (default); 0: always the int64 kernel

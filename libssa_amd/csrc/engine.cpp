@@ -64,6 +64,8 @@ void DeviceDB::release() {
     rowbuf_q_cap = 0;
     dfree(d_rowbuf2);
     d_rowbuf2 = nullptr;
+    dfree(d_rowbuf3);
+    d_rowbuf3 = nullptr;
     for (auto& pr : prs) {
         dfree(pr.d);
         pr = PairRows();
@@ -761,13 +763,13 @@ static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
 }
 
 // strip parts of a pair-kernel launch of T strips (StripArgs::nparts; at
-// most two: pair_kernel.h store_row's coherence argument).  Auto: two parts for
-// groups of at least 4 strips -- C2 (9 strips) +1.1 %, C3 (13) +1.1 %, the
-// reference's benchmark shape (11) +6-8 %, q = 200 (5) +1 %; q = 100 (3)
-// -2.3 % (profiles/r03/parts_sweep.txt)
+// most three: one row buffer per part, pair_kernel.h store_row's coherence
+// argument).  Auto: two parts for groups of at least 4 strips -- C2 (9
+// strips) +1.1 %, C3 (13) +1.1 %, the reference's benchmark shape (11)
+// +6-8 %, q = 200 (5) +1 %; q = 100 (3) -2.3 % (profiles/r03/parts_sweep.txt)
 static uint32_t strip_parts(uint32_t T) {
     const int o = cfg().pair_parts;
-    const uint32_t p = o == 0 ? (T >= 4 ? 2u : 1u) : (o > 1 ? 2u : 1u);
+    const uint32_t p = o == 0 ? (T >= 4 ? 2u : 1u) : o >= 3 ? 3u : o == 2 ? 2u : 1u;
     return std::min(p, T);
 }
 
@@ -1740,6 +1742,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 const size_t nqf = fused ? V : 1;
                 uint32_t parts = no_parts ? 1u : strip_parts(T);
+                if (fused) parts = std::min(parts, 2u);   // (a fused batch's layout holds two row buffers)
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
                     const uint32_t ps = (T + parts - 1) / parts;
@@ -1761,7 +1764,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     // this launch's handoff flag value (no per-launch clearing:
                     // older launches left smaller or different values; never 0,
                     // the value of fresh memory)
-                    if (++D.part_epoch == 0) ++D.part_epoch;
+                    // (a multiple of 4: part q's flag is part_epoch + q)
+                    D.part_epoch += 4;
+                    if (D.part_epoch < 4) D.part_epoch = 4;
                     b.part_epoch = D.part_epoch;
                     b.nparts = parts;
                     b.part_strips = ps;
@@ -1782,6 +1787,13 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                             check(hipMalloc((void**)&D.d_rowbuf2, (size_t)D.nblocks * 4096), "second row buffer");
                         }
                         b.rowbuf2 = D.d_rowbuf2;
+                        if (parts > 2) {
+                            if (!D.d_rowbuf3) {
+                                if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                                check(hipMalloc((void**)&D.d_rowbuf3, (size_t)D.nblocks * 4096), "third row buffer");
+                            }
+                            b.rowbuf3 = D.d_rowbuf3;
+                        }
                     }
                     parts_used = true;
                 }

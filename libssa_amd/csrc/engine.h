@@ -102,6 +102,7 @@ struct DeviceDB {
     uint32_t* d_smax = nullptr;
     size_t smax_cap = 0;
     uint4* d_rowbuf2 = nullptr;           // part 1's row buffer (StripArgs::rowbuf2), as d_rowbuf
+    uint4* d_rowbuf3 = nullptr;           // part 2's (StripArgs::rowbuf3; three parts only)
     // fused batches (StripArgs::nq): one row buffer per query
     uint8_t* d_rowbuf_q = nullptr;
     size_t rowbuf_q_cap = 0;

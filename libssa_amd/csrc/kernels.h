@@ -63,20 +63,22 @@ struct StripArgs {
     // units of all groups' first parts come first (longest groups first),
     // then all second parts.  A part waits until its group's previous part
     // is done (part_done[quad]); the handoff boundary crosses workgroups,
-    // maybe XCDs, through device-scope stores, and part 1 keeps its own
-    // boundaries in rowbuf2 (pair_kernel.h store_row: the coherence argument,
-    // which limits nparts to 2); the SW running maximum travels in
+    // maybe XCDs, through device-scope stores, and part p keeps its own
+    // boundaries in its own buffer -- rowbuf (part 0), rowbuf2, rowbuf3 --
+    // so no buffer is written from two XCDs (pair_kernel.h store_row: the
+    // coherence argument; at most 3 parts); the SW running maximum travels in
     // part_smax (one dword per lane).  The launch's last units are then
-    // the shortest groups' second parts -- a fraction of a whole group's work
+    // the shortest groups' last parts -- a fraction of a whole group's work
     // -- so the SIMDs drain closer together.
     // nparts 1: whole groups, no carry.
     uint32_t nparts, part_strips, nquads;
-    uint32_t* part_done;       // [nquads] part_epoch once the quad's first part is done (never cleared)
-    uint32_t part_epoch;       // this launch's flag value (differs from every earlier launch's)
+    uint32_t* part_done;       // [nquads] part_epoch + q once the quad's part q is done (never cleared)
+    uint32_t part_epoch;       // this launch's flag base: a multiple of 4, above every earlier launch's values
     uint32_t* part_smax;       // [ngroups * 64]
     uint32_t* part_err;        // set when a wait timed out (the host then runs the search again without parts)
     uint32_t part_wait;        // bound of that wait, s_memrealtime ticks (100 MHz)
     uint4* rowbuf2;            // part 1's own strip boundaries (same layout as rowbuf)
+    uint4* rowbuf3;            // part 2's (nparts 3)
     // pair_kernel: several queries of one plan in one launch (a batch of
     // short queries, ssa_amd_search_batch): unit order part, quad (longest
     // first), query; query qi reads its tables at qpt / qpt_tail + qi *

@@ -76,18 +76,20 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const u32x4 lds_u4;
 
-// Strip parts (StripArgs::nparts = 2) hand a group's boundary rows from the
-// workgroup of part 0 (XCD A) to that of part 1 (maybe XCD B; the XCDs' L2s
-// are not coherent).  Part 0 keeps its strip boundaries in the row buffer as
-// usual, but writes its LAST boundary -- the one part 1 reads -- with
-// device-scope 16-byte stores (a buffer store with the sc1 bit: write-through
-// past A's L2, full lines), then waits for them (vmcnt 0) before the flag.
-// Part 1 reads that boundary with ordinary loads (B's L1/L2 never held these
-// lines in this kernel: dispatch invalidates them) and keeps its own
-// boundaries in a second row buffer (StripArgs::rowbuf2), so no dirty line
-// of the first buffer left in A's L2 can ever be written back over newer
+// Strip parts (StripArgs::nparts = 2 or 3) hand a group's boundary rows from
+// the workgroup of part p-1 (XCD A) to that of part p (maybe XCD B; the XCDs'
+// L2s are not coherent).  Part p-1 keeps its strip boundaries in its row
+// buffer as usual, but writes its LAST boundary -- the one part p reads --
+// with device-scope 16-byte stores (a buffer store with the sc1 bit:
+// write-through past A's L2, full lines), then waits for them (vmcnt 0)
+// before the flag.  Part p reads that boundary with ordinary loads (B's L1/L2
+// never held these lines in this kernel: dispatch invalidates them, and only
+// part p-1 wrote them) and keeps its own boundaries in a buffer of its own
+// (rowbuf2 for part 1, rowbuf3 for part 2), so no dirty line of another
+// part's buffer left in another XCD's L2 can ever be written back over newer
 // data.  No cache-wide writeback/invalidate (those stalled every XCD: -3 %
-// on C2); the row-buffer traffic is unchanged.  Two parts at most.
+// on C2); the row-buffer traffic is unchanged.  One buffer per part, so at
+// most three parts.
 __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint4 v, bool dev) {
     const u32x4 x = {v.x, v.y, v.z, v.w};
     if (dev) __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff, soff, 16 /* sc1 */);
@@ -157,7 +159,7 @@ pair_kernel(const StripArgs a) {
             if (threadIdx.x == 0) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (__hip_atomic_load(a.part_done + (size_t)wg * nqs + qi, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) != a.part_epoch) {
+                                         __HIP_MEMORY_SCOPE_AGENT) != a.part_epoch + part - 1) {
                     if (__builtin_amdgcn_s_memrealtime() - t0 >= a.part_wait) {
                         __hip_atomic_store(a.part_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -186,17 +188,19 @@ pair_kernel(const StripArgs a) {
     const uint32_t nquads = gd.ncols >> 2;
     const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint4* resp = a.res + (size_t)gd.blk * 64 + lane;
-    // row buffers: rb0 (part 0, and every strip without parts), rb1 (part
-    // 1's own boundaries); rbr / rbw: where the current strip reads its top
-    // boundary and writes its bottom one
+    // row buffers: part p's own boundaries in rowbuf / rowbuf2 / rowbuf3
+    // (rowbuf also for every strip without parts); rbr / rbw: where the
+    // current strip reads its top boundary (part p > 0 first: part p-1's
+    // buffer, the handoff) and writes its bottom one
     // (quad q of a group at byte q * 1024 + lane * 16, as the pair-row stream)
-    const __amdgpu_buffer_rsrc_t rb0 = group_rsrc(a.rowbuf + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256);
-    const __amdgpu_buffer_rsrc_t rb1 =
-        a.nparts > 1 ? group_rsrc(a.rowbuf2 + qi * a.q_rowbuf_stride + (size_t)gd.blk * 256) : rb0;
-    __amdgpu_buffer_rsrc_t rbr = rb0;
-    __amdgpu_buffer_rsrc_t rbw = part > 0 ? rb1 : rb0;
+    // (scalar selects: part is wave-uniform)
+    const size_t roff = qi * a.q_rowbuf_stride + (size_t)gd.blk * 256;
+    const uint4* const own = part == 0 ? a.rowbuf : part == 1 ? a.rowbuf2 : a.rowbuf3;
+    const uint4* const prev = part <= 1 ? a.rowbuf : a.rowbuf2;
+    __amdgpu_buffer_rsrc_t rbr = group_rsrc(prev + roff);
+    __amdgpu_buffer_rsrc_t rbw = group_rsrc(own + roff);
     const uint32_t lane16 = (uint32_t)lane * 16;
-    // part 0's last strip stores its boundary at device scope (the handoff)
+    // a non-last part's last strip stores its boundary at device scope (the handoff)
     bool handoff = false;
     // the pair-row stream: per 16-column block two octs of 64 lanes x 16 B,
     // eight 16-bit offsets (LDS byte offset / 16) per lane and oct
@@ -502,7 +506,7 @@ pair_kernel(const StripArgs a) {
     const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
     const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
     for (uint32_t s = s0; s < min(s1, a.nstrips); s++) {
-        handoff = a.nparts > 1 && part == 0 && s + 1 == s1;
+        handoff = part + 1 < a.nparts && s + 1 == s1;
         strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, qpt + (size_t)s * prow * prow * NP);
     }
     if (NPT > 0 && s1 == T) {
@@ -519,7 +523,7 @@ pair_kernel(const StripArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, a.part_epoch, __ATOMIC_RELAXED,
+            __hip_atomic_store(a.part_done + (size_t)wg * nqs + qi, a.part_epoch + part, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         return;
     }

@@ -369,7 +369,8 @@ def test_strip_parts_keep_scores(algo, qlen):
     """pair_kernel with each group's strips split into dependent work units
     (option "pair_parts": all groups' first parts, then the second, ...; the
     strip boundary rows and SW running maxima cross workgroups): every score
-    equals the oracle's with two parts (more are clamped to two), with and
+    equals the oracle's with two and three parts (more are clamped to three;
+    each part keeps its boundaries in a row buffer of its own), with and
     without long_kernel groups and start-order tickets."""
     rng = np.random.default_rng(qlen)
     q = syn.protein_query(qlen, 77 + qlen)
@@ -386,7 +387,8 @@ def test_strip_parts_keep_scores(algo, qlen):
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
         try:
-            for parts, lg, ticket in ((2, -1, 1), (2, 0, 1), (50, 1, 1), (2, 2, 0), (1, -1, 1)):
+            for parts, lg, ticket in ((2, -1, 1), (2, 0, 1), (3, -1, 1), (3, 0, 1), (50, 1, 1), (2, 2, 0),
+                                      (3, 2, 0), (1, -1, 1)):
                 S.set_option("pair_parts", parts)
                 S.set_option("long_groups", lg)
                 S.set_option("pair_ticket", ticket)
@@ -426,11 +428,12 @@ def test_strip_part_wait_timeout_reruns_without_parts(algo):
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
         qs = [S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q[:n])) for n in (300, 290, 299)]
         try:
-            S.set_option("pair_parts", 2)
             S.set_option("part_wait_us", 0)
-            sc, ids = _full_scores(qq, algo, len(keep))
-            assert (ids == keep).all() and (sc == exp).all(), np.nonzero(sc != exp)[0][:10]
-            assert S.stats()["part_retries"] == 1
+            for parts in (3, 2):
+                S.set_option("pair_parts", parts)
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all() and (sc == exp).all(), (parts, np.nonzero(sc != exp)[0][:10])
+                assert S.stats()["part_retries"] == 1, parts
             top = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
             assert top == po.topk(exp, keep.astype(np.uint64), 10)
             batch = S.search_batch(qs, algo, 10)

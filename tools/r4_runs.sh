@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments, one function per run (the command lines the round-4
 # profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
-#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
+#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
 set -o pipefail
 
 r4_ab() (
@@ -294,6 +294,40 @@ r4_np_sweep() (
       run c5s_np$np_ --config c5 --seqs 1000000 --steps 3 --pair-np $np_ || exit 1
       run c2_np$np_ --config c2 --pair-np $np_ || exit 1
     done
+)
+
+r4_parts3() (
+    # three strip parts: the parts tests, then pair_parts 3 against the default (2) on five shapes
+    mkdir -p gpurun_out/r4/parts3
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -m gpu \
+        -k "strip_part or batch_fused" > gpurun_out/r4/parts3/tests.log 2>&1 || { tail -30 gpurun_out/r4/parts3/tests.log; exit 1; }
+    tail -1 gpurun_out/r4/parts3/tests.log
+    run() {  # name, args
+      local n=$1; shift
+      timeout -k 10 300 python bench.py --steps ${STEPS:-15} --warmup 3 --no-north-star --no-cpu-baseline "$@" > gpurun_out/r4/parts3/$n.json 2> gpurun_out/r4/parts3/$n.err || { tail -20 gpurun_out/r4/parts3/$n.err; return 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/r4/parts3/$n.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['kernel']['kernel_gcups'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+    }
+    for i in 1 2; do
+      for cfg in ref sprot c2 c3; do
+        run ${cfg}_p2_$i --config $cfg && run ${cfg}_p3_$i --config $cfg --option pair_parts=3 || exit 1
+      done
+    done
+    run c5s_p2 --config c5 --seqs 1000000 --steps 3 && run c5s_p3 --config c5 --seqs 1000000 --steps 3 --option pair_parts=3 || exit 1
+)
+
+r4_parts3b() (
+    # pair_parts 3 vs 2, repeated on the headline (C2) and the north-star DB
+    mkdir -p gpurun_out/r4/parts3b
+    run() {  # name, args
+      local n=$1; shift
+      timeout -k 10 300 python bench.py --warmup 3 --no-north-star --no-cpu-baseline "$@" > gpurun_out/r4/parts3b/$n.json 2> gpurun_out/r4/parts3b/$n.err || { tail -20 gpurun_out/r4/parts3b/$n.err; return 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/r4/parts3b/$n.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['kernel']['kernel_gcups'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+    }
+    for i in 1 2 3 4; do
+      run c2_p2_$i --steps 20 --option pair_parts=2 && run c2_p3_$i --steps 20 --option pair_parts=3 || exit 1
+    done
+    run ns_p2 --config north_star --steps 4 --option pair_parts=2 && run ns_p3 --config north_star --steps 4 --option pair_parts=3 || exit 1
+    run c4s_p2 --config c4 --seqs 1250000 --steps 15 --option pair_parts=2 && run c4s_p3 --config c4 --seqs 1250000 --steps 15 --option pair_parts=3 || exit 1
 )
 
 name=${1:?usage: tools/r4_runs.sh <name> [args]}; shift
