@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments, one function per run (the command lines the round-4
 # profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
-#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
+#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b parts3c pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
 set -o pipefail
 
 r4_ab() (
@@ -328,6 +328,21 @@ r4_parts3b() (
     done
     run ns_p2 --config north_star --steps 4 --option pair_parts=2 && run ns_p3 --config north_star --steps 4 --option pair_parts=3 || exit 1
     run c4s_p2 --config c4 --seqs 1250000 --steps 15 --option pair_parts=2 && run c4s_p3 --config c4 --seqs 1250000 --steps 15 --option pair_parts=3 || exit 1
+)
+
+r4_parts3c() (
+    # pair_parts 3 vs 2 on the C5 shapes (209 strips per group)
+    mkdir -p gpurun_out/r4/parts3c
+    run() {  # name, args
+      local n=$1; shift
+      timeout -k 10 600 python bench.py --no-north-star --no-cpu-baseline "$@" > gpurun_out/r4/parts3c/$n.json 2> gpurun_out/r4/parts3c/$n.err || { tail -20 gpurun_out/r4/parts3c/$n.err; return 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/r4/parts3c/$n.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['kernel']['kernel_gcups'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+    }
+    for i in 1 2; do
+      run c5share_p2_$i --config c5 --seqs 6250000 --steps 3 --warmup 1 --option pair_parts=2 &&
+      run c5share_p3_$i --config c5 --seqs 6250000 --steps 3 --warmup 1 --option pair_parts=3 || exit 1
+    done
+    run c5_p2 --config c5 --steps 2 --warmup 1 --option pair_parts=2 && run c5_p3 --config c5 --steps 2 --warmup 1 --option pair_parts=3 || exit 1
 )
 
 name=${1:?usage: tools/r4_runs.sh <name> [args]}; shift
