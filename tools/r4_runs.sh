@@ -198,6 +198,8 @@ r4_ref_gap() (
 )
 
 r4_sprot() (
+    # (historical: the rare-merge runs of profiles/r04/rare_merge; option rare_merge_ppm
+    # left with the feature)
     mkdir -p gpurun_out/r4
     timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "rare_merge or sprot or sp25 or u28 or residue_classes" > gpurun_out/r4/rm_tests.log 2>&1 || { tail -60 gpurun_out/r4/rm_tests.log; exit 1; }
     tail -2 gpurun_out/r4/rm_tests.log
@@ -208,6 +210,8 @@ r4_sprot() (
 )
 
 r4_sprot2() (
+    # (historical: the rare-merge runs of profiles/r04/rare_merge; option rare_merge_ppm
+    # left with the feature)
     mkdir -p gpurun_out/r4
     timeout -k 10 300 python tools/sprot_diag.py 5000 0 5000 0 > gpurun_out/r4/sprot_diag2.log 2>&1 || { tail -20 gpurun_out/r4/sprot_diag2.log; exit 1; }
     grep ppm gpurun_out/r4/sprot_diag2.log
@@ -219,6 +223,8 @@ r4_sprot2() (
 )
 
 r4_sprot3() (
+    # (historical: the rare-merge runs of profiles/r04/rare_merge; option rare_merge_ppm
+    # left with the feature)
     # where the reference-shape gap goes: alphabet, tail, rare merge (SW and NW), same box alternating
     mkdir -p gpurun_out/r4/sprot3
     run() {  # name, args

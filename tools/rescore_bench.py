@@ -3,7 +3,7 @@
 tier (long_kernel over the overflow list) against the int64 wide_kernel."""
 import os, sys, tempfile, time
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import libssa_amd as S
 from libssa_amd import synthetic as syn

@@ -1,7 +1,9 @@
-"""One sprot-shape search with and without the rare merge: stats per search."""
+"""One sprot-shape search with and without the rare merge: stats per search.
+(Historical: option "rare_merge_ppm" was removed with the feature, DESIGN.md §3.1;
+this produced profiles/r04/rare_merge/diag.txt.)"""
 import json, os, sys, tempfile
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import libssa_amd as S
 from libssa_amd import synthetic as syn, workloads as W
