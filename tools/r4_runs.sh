@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments, one function per run (the command lines the round-4
 # profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
-#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b parts3c pmc_more post_check ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
+#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b parts3c pmc_more post_check prio ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
 set -o pipefail
 
 r4_ab() (
@@ -349,6 +349,19 @@ r4_parts3c() (
       run c5share_p3_$i --config c5 --seqs 6250000 --steps 3 --warmup 1 --option pair_parts=3 || exit 1
     done
     run c5_p2 --config c5 --steps 2 --warmup 1 --option pair_parts=2 && run c5_p3 --config c5 --steps 2 --warmup 1 --option pair_parts=3 || exit 1
+)
+
+r4_prio() (
+    # option pair_prio_groups (raised wave priority for the longest pair groups): 0 (default) vs -1 vs 512
+    mkdir -p gpurun_out/r4/prio
+    run() {  # name, args
+      local n=$1; shift
+      timeout -k 10 300 python bench.py --steps 15 --warmup 3 --no-north-star --no-cpu-baseline "$@" > gpurun_out/r4/prio/$n.json 2> gpurun_out/r4/prio/$n.err || { tail -20 gpurun_out/r4/prio/$n.err; return 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/r4/prio/$n.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['kernel']['kernel_gcups'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+    }
+    for cfg in ref sprot c2; do
+      for pr in 0 -1 512 0; do run ${cfg}_pr${pr}_$RANDOM --config $cfg --option pair_prio_groups=$pr || exit 1; done
+    done
 )
 
 name=${1:?usage: tools/r4_runs.sh <name> [args]}; shift
