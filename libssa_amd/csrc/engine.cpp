@@ -1743,6 +1743,16 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const size_t nqf = fused ? V : 1;
                 uint32_t parts = no_parts ? 1u : strip_parts(T);
                 if (fused) parts = std::min(parts, 2u);   // (a fused batch's layout holds two row buffers)
+                if (parts > 2 && !D.d_rowbuf3 && D.ngroups > long_groups) {
+                    // the third part's row buffer (4 B per residue slot); without
+                    // the memory for it the search runs two parts
+                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                    if (hipMalloc((void**)&D.d_rowbuf3, (size_t)D.nblocks * 4096) != hipSuccess) {
+                        (void)hipGetLastError();
+                        D.d_rowbuf3 = nullptr;
+                        parts = 2;
+                    }
+                }
                 if (parts > 1 && D.ngroups > long_groups) {
                     const uint32_t quads = (D.ngroups - long_groups + kPairWaves - 1) / kPairWaves;
                     const uint32_t ps = (T + parts - 1) / parts;
@@ -1787,13 +1797,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                             check(hipMalloc((void**)&D.d_rowbuf2, (size_t)D.nblocks * 4096), "second row buffer");
                         }
                         b.rowbuf2 = D.d_rowbuf2;
-                        if (parts > 2) {
-                            if (!D.d_rowbuf3) {
-                                if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
-                                check(hipMalloc((void**)&D.d_rowbuf3, (size_t)D.nblocks * 4096), "third row buffer");
-                            }
-                            b.rowbuf3 = D.d_rowbuf3;
-                        }
+                        if (parts > 2) b.rowbuf3 = D.d_rowbuf3;
                     }
                     parts_used = true;
                 }
