@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments, one function per run (the command lines the round-4
 # profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
-#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep pack_trace pmc_all np_sweep parts3 parts3b parts3c pmc_more post_check prio ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
+#   bash tools/r4_runs.sh <name> [args]      names: ab ab_w6 api_trace bench_ns c5 final full gpu_tests long_sweep medians pack_trace pmc_all np_sweep parts3 parts3b parts3c pmc_more post_check prio ref_gap sprot sprot2 sprot3 sync_ab tl tl2 tl_jag
 set -o pipefail
 
 r4_ab() (
@@ -361,6 +361,20 @@ r4_prio() (
     }
     for cfg in ref sprot c2; do
       for pr in 0 -1 512 0; do run ${cfg}_pr${pr}_$RANDOM --config $cfg --option pair_prio_groups=$pr || exit 1; done
+    done
+)
+
+r4_medians() (
+    # the verdict's measure: median of 5 x 20-step runs, sprot / ref / C2, final build
+    mkdir -p gpurun_out/r4/medians
+    for cfg in sprot ref c2; do
+      for i in 1 2 3 4 5; do
+        timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-north-star --no-cpu-baseline > gpurun_out/r4/medians/${cfg}_$i.json 2> gpurun_out/r4/medians/${cfg}_$i.err || { tail -20 gpurun_out/r4/medians/${cfg}_$i.err; exit 1; }
+      done
+      python -c "
+import json, statistics as st
+v=[json.loads(open('gpurun_out/r4/medians/${cfg}_%d.json' % i).read().strip().splitlines()[-1]) for i in range(1, 6)]
+print('$cfg', 'e2e median', st.median(d['value'] for d in v), 'kernel median', st.median(d['kernel']['kernel_gcups'] for d in v), [round(d['value']) for d in v])"
     done
 )
 
