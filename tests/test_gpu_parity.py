@@ -1340,6 +1340,7 @@ def test_search_batch_fused_launch(algo):
         try:
             for qlens, opts in (([30] * 8, {}), ([97, 104, 100, 99, 101, 98, 103, 102], {}),
                                 ([97, 104, 100, 99, 101, 98, 103, 102], {"pair_parts": 2}),
+                                ([97, 104, 100, 99, 101, 98, 103, 102], {"pair_parts": 3}),
                                 ([30, 29, 31, 28, 27, 26, 30, 25], {"long_groups": 1}),
                                 ([5] * 3, {})):
                 qs = [S.init_sequence_fasta(S.READ_FROM_STRING,
@@ -1348,13 +1349,18 @@ def test_search_batch_fused_launch(algo):
                 for k, v in opts.items():
                     S.set_option(k, v)
                 for k in (1, 10, 64):
-                    exp = [[(h["score"], h["id"]) for h in fn(q, k, 16)] for q in qs]
+                    exp, ncand = [], 0
+                    for q in qs:
+                        exp.append([(h["score"], h["id"]) for h in fn(q, k, 16)])
+                        ncand += S.stats()["filter_candidates"]
                     S.set_option("batch_fuse", 0)
                     assert S.search_batch(qs, algo, k) == exp, (qlens, opts, k, "unfused")
                     assert S.stats()["kernel_launches"] == len(qs)
                     S.set_option("batch_fuse", 1)
                     got = S.search_batch(qs, algo, k)
                     assert got == exp, (qlens, opts, k)
+                    # every query's own filter pass: the same candidates as alone
+                    assert S.stats()["filter_candidates"] == ncand, (qlens, opts, k)
                     # NW with long_kernel groups and counters keeps one launch per query
                     unfusable = algo == S.NW and "long_groups" in opts
                     assert S.stats()["kernel_launches"] == (len(qs) if unfusable else 1), (qlens, opts)
