@@ -1098,6 +1098,16 @@ def test_multiview_device_filter_matches_full_scan(mode):
                     log_full = S.search(qq, algo, 9, 16, S.LOG)
                     S.set_option("no_filter", 0)
                     assert S.search(qq, algo, 9, 16, S.LOG) == log_full
+                    # the filter's bounds over the chunk-interleaved order (its
+                    # d_order indirection): with k >= all (view, entry) pairs the
+                    # insertion log is every score in insertion order
+                    total = S.stats()["entries"] * len(S.query_views(qq))
+                    order_sc = np.array([h[0] for h in S.search(qq, algo, total, 16, S.LOG, cap=total + 8)],
+                                        np.int64)
+                    assert len(order_sc) == total
+                    for k in (1, 10, 64):
+                        fn(qq, k, 16)
+                        assert S.stats()["filter_candidates"] == _filter_candidates(order_sc, k), (mode, chunk, k)
                 S.free_sequence(qq)
     finally:
         S.set_option("no_filter", 0)
