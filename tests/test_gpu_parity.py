@@ -999,8 +999,8 @@ def _filter_candidates(sc, k):
     return int(np.count_nonzero(sc > np.maximum(t_block[e // 4096], t_local[e // 64])))
 
 
-@pytest.mark.parametrize("n,pattern", [(90000, "random"), (90000, "rising"), (700000, "random"),
-                                       (700000, "falling")])
+@pytest.mark.parametrize("n,pattern", [(100, "random"), (4097, "rising"), (90000, "random"), (90000, "rising"),
+                                       (700000, "random"), (700000, "falling")])
 def test_device_filter_candidate_count_is_exact(n, pattern):
     """The filter's lane moves (DPP, v_permlane16/32_swap) and its
     cross-wave scan of the block summaries must give exactly the bounds the
