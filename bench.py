@@ -194,9 +194,12 @@ def host_cpu():
 def cpu_baseline(codes, off, q, M, args):
     """The reference's own AVX2 int16 kernel (search_16_chunk ->
     search_16_avx2_sw, compiled from its sources into oracle/_ref) timed on
-    the host's CPU share (every core of it) over a bounded sample, and on one
-    thread; falls back to the int64 oracle port when the reference build is
-    absent."""
+    the host's CPU share (every core of it) and on one thread, each as the
+    median of 5 runs after 1 warm-up run.  The all-core
+    figure searches the whole DB unless one run would exceed --cpu-seconds/3
+    (C2: the whole 1 M sequences, ~0.4 s a run on 16 threads); the one-thread
+    figure the first sequences worth ~--cpu-seconds/7.5 per run.  Falls back to
+    the int64 oracle port when the reference build is absent."""
     from oracle import pyoracle as po
     cores, model, share = host_cpu()
     algo = 0 if args.algo == "sw" else 1
@@ -209,21 +212,23 @@ def cpu_baseline(codes, off, q, M, args):
         kname = "AVX2 int8 search_8 cascade" if args.width == 8 else "AVX2 int16 search_16_chunk"
 
         def run(threads, seconds):
-            # sample sized to ~seconds at a conservative 8 GCUPS per thread
-            sample = int(min(n, max(1000, seconds * 8e9 * threads / cells_per_seq)))
+            # sample sized to ~seconds per run at ~20 GCUPS per thread
+            sample = int(min(n, max(1000, seconds * 20e9 * threads / cells_per_seq)))
             soff = off[:sample + 1]
             _, _, _, secs = po.ref_run(mode, algo, q, None, M, args.gap_open, args.gap_extend,
-                                       k=args.k, threads=threads, repeat=2, db_off=(codes, soff))
+                                       k=args.k, threads=threads, repeat=6, db_off=(codes, soff), times=True)
             cells = float(soff[-1]) * len(q)
-            return cells / secs / 1e9, sample, cells
+            return cells / float(np.median(secs[1:])) / 1e9, sample, cells, secs
 
-        v, sample, cells = run(cores, args.cpu_seconds * 0.6)
-        v1, sample1, _ = run(1, args.cpu_seconds * 0.3)
+        v, sample, cells, secs = run(cores, args.cpu_seconds / 3)
+        v1, sample1, cells1, secs1 = run(1, args.cpu_seconds / 7.5)
+        whole = "the whole DB" if sample == n else f"first {sample} of {n} DB sequences"
         return {"value": v, "unit": "GCUPS", "cores": cores, "kind": "reference",
                 "one_thread_gcups": v1, "cpu_model": model, "host_share": share,
-                "sample": f"first {sample} of {n} DB sequences ({cells:.3g} cells), reference {kname} "
-                          f"on {cores} threads (best of 2), chunk 1000, k={args.k}; one thread: "
-                          f"first {sample1} sequences"}
+                "run_seconds": [round(x, 4) for x in secs], "one_thread_run_seconds": [round(x, 4) for x in secs1],
+                "sample": f"{whole} ({cells:.3g} cells), reference {kname} on {cores} threads, median of 5 "
+                          f"runs after 1 warm-up, chunk 1000, k={args.k}; one thread: first {sample1} of {n} "
+                          f"sequences ({cells1:.3g} cells), median of 5 after 1 warm-up"}
     po.build(quiet=True)
     sample = 2000
     soff = off[:sample + 1]
@@ -522,21 +527,32 @@ def timed_steps(S, job, sh, w, steps, warmup, k):
     """W untimed warm-up steps, then exactly K steps between barrier +
     synchronize on both sides; the max over ranks of the elapsed time."""
     algo = S.SW if w.algo == "sw" else S.NW
+    # N > 1: the host clock around each step's search and gather, on every
+    # rank (two perf_counter reads per step; they add nothing measurable)
+    split = {"search_s": [], "gather_s": []}
 
     def step():
         if job.world == 1:
             # the public sw_align / nw_align + free_alignment (libssa.h)
             return S.align_scores(sh.qq, k, w.width, algo)
+        t0 = time.perf_counter()
         log = S.search(sh.qq, algo, k, w.width, S.LOG)
+        t1 = time.perf_counter()
         if job.native:
-            return S.gather_logs(log, k)
-        from libssa_amd.dist import global_topk
-        return global_topk(log, k, job.dist, job.rank, job.world, job.dev)
+            res = S.gather_logs(log, k)
+        else:
+            from libssa_amd.dist import global_topk
+            res = global_topk(log, k, job.dist, job.rank, job.world, job.dev)
+        split["search_s"].append(t1 - t0)
+        split["gather_s"].append(time.perf_counter() - t1)
+        return res
 
     for _ in range(warmup):
         step()
     if job.native and job.gather_checked is None:
         check_native_gather(S, job, sh.qq, algo, k, w.width)
+    split["search_s"].clear()
+    split["gather_s"].clear()
     # the timed region holds only the searches (and at N > 1 the gather):
     # the library's running totals are read once on each side of it
     st0 = S.stats()
@@ -557,7 +573,53 @@ def timed_steps(S, job, sh, w, steps, warmup, k):
     # (host-side breakdown: the last search's)
     for f in ("wide_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms", "replay_ms"):
         avg[f] = st[f]
-    return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=st, avg=avg)
+    ranks = rank_split(job, sh, avg, split, elapsed / steps) if job.world > 1 else None
+    return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=st, avg=avg, ranks=ranks)
+
+
+def rank_split(job, sh, avg, split, step_s):
+    """N > 1: where a step's time goes, rank by rank -- so a scaling run
+    explains its own result (imbalance, host overhead or the collective).
+    Every rank contributes (kernel ms, search ms, gather median / max ms,
+    residues, cells) through one all-gather after the timed region; rank 0
+    reports the lists and:
+      kernel_balance_efficiency = (sum of rank cells / max rank kernel time)
+                                  / sum of rank kernel rates  (1.0: no rank waits
+                                  on the slowest kernel)
+      residue_imbalance = max rank residues / mean rank residues
+      step_split_ms: the slowest kernel, the search call's host overhead on that
+                     rank, the gather (median and max over ranks and steps) and
+                     the rest of the step (barrier skew between ranks)."""
+    import torch
+    g = np.array(split["gather_s"]) * 1e3
+    s = np.array(split["search_s"]) * 1e3
+    mine = torch.tensor([avg["kernel_ms"], avg["search_ms"], float(np.median(s)) if s.size else 0.0,
+                         float(np.median(g)) if g.size else 0.0, float(g.max()) if g.size else 0.0,
+                         float(sh.residues), float(sh.cells_local), float(sh.seqs)],
+                        dtype=torch.float64, device=job.dev)
+    rows = [torch.empty_like(mine) for _ in range(job.world)]
+    job.dist.all_gather(rows, mine)
+    R = np.array([r.cpu().numpy() for r in rows])
+    kms, sms, step_search, gmed, gmax, res, cells, seqs = R.T
+    rate = cells / (kms * 1e-3)
+    slow = int(np.argmax(kms))
+    return {
+        "kernel_ms": [round(x, 4) for x in kms], "search_ms": [round(x, 4) for x in sms],
+        "gather_ms_median": [round(x, 4) for x in gmed], "gather_ms_max": [round(x, 4) for x in gmax],
+        "seqs": [int(x) for x in seqs], "residues": [int(x) for x in res],
+        "kernel_gcups": [round(x / 1e9, 2) for x in rate],
+        "kernel_ms_min": round(float(kms.min()), 4), "kernel_ms_max": round(float(kms.max()), 4),
+        "kernel_ms_argmax": slow,
+        "search_ms_min": round(float(sms.min()), 4), "search_ms_max": round(float(sms.max()), 4),
+        "search_ms_argmax": int(np.argmax(sms)),
+        "gather_ms": {"median": round(float(np.median(gmed)), 4), "max": round(float(gmax.max()), 4)},
+        "kernel_balance_efficiency": round(float(cells.sum() / (kms.max() * 1e-3) / rate.sum()), 4),
+        "residue_imbalance": round(float(res.max() / res.mean()), 5),
+        "step_split_ms": {"step": round(step_s * 1e3, 4), "kernel_max": round(float(kms.max()), 4),
+                          "search_host_overhead": round(float(sms[slow] - kms[slow]), 4),
+                          "gather_median": round(float(np.median(gmed)), 4),
+                          "rest": round(step_s * 1e3 - float(sms[slow]) - float(np.median(gmed)), 4)},
+    }
 
 
 def fixture_match(w, sh, res, k, world):
@@ -617,12 +679,15 @@ def north_star(S, args, job):
                   "kernel_gcups": round(kernel_gcups, 2)},
         "kernel_ms_max_over_ranks": round(job.max(kms), 4),
         "kernel_gcups_min_over_ranks": round(job.min(kernel_gcups), 2),
+        "search_ms_rank0": round(t.avg["search_ms"], 4),
         "hbm": {"algorithmic_bytes_rank0": float(t.st["kernel_bytes"]),
                 "frac_of_peak": float(t.st["kernel_bytes"]) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "setup_s": round(job.max(sh.setup_s), 1),
         "top_hit": list(map(int, t.res[0][:2])) if t.res else None,   # (rank 0: the gathered result)
         "gather": ("ssa_amd_gather_logs (RCCL)" if job.native else "torch.distributed") if job.world > 1 else None,
     }
+    if t.ranks is not None:
+        rec["ranks_split"] = t.ranks
     m = fixture_match(w, sh, t.res, args.k, job.world)
     if m is not None:
         rec["topk_vs_reference"] = m
@@ -771,6 +836,8 @@ def main():
         "rccl_ranks": job.rccl_ranks,
         "launcher": os.environ.get("SSA_BENCH_LAUNCHER", "torchrun" if world > 1 else None),
     }
+    if t.ranks is not None:
+        out["ranks_split"] = t.ranks
     if ranks_per_gpu > 1:
         out["ranks"] = world
         out["rehearsal"] = rehearsal_label(world, args.n_gpus, backend)

@@ -70,6 +70,10 @@ typedef struct {
     double total_search_ms;  /* sum of search_ms */
     uint64_t filter_candidates;  /* scores of the last search the device top-k filter let through to
                                     the host (every score when it ran without the filter) */
+    double gather_ms;        /* host wall time of this rank's last ssa_amd_gather_logs (staging, the
+                                collective, rank 0's replay) */
+    uint32_t gather_rounds;  /* 1: the slot gather alone; 2: this rank also sent (or rank 0 received)
+                                log rows beyond the 512-row slot point to point */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -167,9 +171,10 @@ size_t ssa_amd_replay( const ssa_hit_t * log, size_t n, size_t hitcount, ssa_hit
  *   every rank:    ssa_amd_set_device(local GPU); ssa_amd_dist_init(rank, world, id)
  *   every search:  n = ssa_amd_search(q, algo, k, width, SSA_AMD_LOG, log, cap);
  *                  c = ssa_amd_gather_logs(log, n, k, out)   (collective)
- * ssa_amd_gather_logs gathers every rank's log over RCCL (one ncclAllGather
- * of fixed 512-row slots; an exact-size ncclGather to rank 0 only when a log
- * is longer) and on rank 0 writes the global sorted top-k to out and returns
+ * ssa_amd_gather_logs gathers every rank's log over RCCL (one ncclGather of
+ * fixed 512-row slots to rank 0; a log longer than its slot sends the rest of
+ * its rows to rank 0 point to point, ncclSend / ncclRecv between those two
+ * ranks only) and on rank 0 writes the global sorted top-k to out and returns
  * its length -- bit-identical to one process searching the whole DB; other
  * ranks return 0.  ssa_amd_dist_init returns 0 on success.
  * ssa_amd_merge_logs is rank 0's merge alone: nlogs logs at rows + r * stride
@@ -186,7 +191,7 @@ int ssa_amd_dist_init( int rank, int world, const void * id );
 /* Test support: the calling THREAD becomes rank `rank` of an in-process
  * group of `world` threads (keyed by `group`), whose collectives exchange
  * through host memory instead of RCCL -- the same slot layout, count rows and
- * exact-size second round as over RCCL.  Released by ssa_amd_dist_finalize on
+ * point-to-point remainder as over RCCL.  Released by ssa_amd_dist_finalize on
  * that thread.  Returns 0 on success. */
 int ssa_amd_dist_init_fake( int rank, int world, int group );
 /* Ranks of the current communicator (ncclCommCount), 0 before init. */

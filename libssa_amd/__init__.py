@@ -69,7 +69,7 @@ class ssa_amd_stats_t(Structure):
                 ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32),
                 ("long_entries", c_uint32), ("long_kernel", ctypes.c_char * 24), ("part_retries", c_uint32),
                 ("total_searches", c_uint64), ("total_kernel_ms", c_double), ("total_search_ms", c_double),
-                ("filter_candidates", c_uint64)]
+                ("filter_candidates", c_uint64), ("gather_ms", c_double), ("gather_rounds", c_uint32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24

@@ -370,7 +370,9 @@ size_t ssa_amd_get_timeline(uint32_t* out, size_t cap) {
 }
 
 void ssa_amd_get_stats(ssa_amd_stats_t* out) {
-    if (out) *out = stats();
+    if (!out) return;
+    *out = stats();
+    dist_overlay_stats(out);      // a fake rank's own gather time (dist.cpp)
 }
 
 int ssa_amd_save_db(const char* path) {
@@ -458,6 +460,9 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
     const double t0 = now_ms();
     double kms = 0;
     uint64_t cells = 0;
+    // the running totals as the batch found them: a lone query below goes
+    // through run_search, which adds itself, so the batch sets them once
+    const ssa_amd_stats_t before = stats();
     // single-device, single-view queries with a small k: pipelined sub-batches
     // (device_search's independent mode) -- the host prepares query i+1 while
     // query i runs, one synchronisation per sub-batch
@@ -537,17 +542,22 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         S.part_retries = retries;
         S.filter_candidates = ncand;
         S.search_ms = now_ms() - t0;
-        S.total_searches += nq;
-        S.total_kernel_ms += kms;
-        S.total_search_ms += S.search_ms;
+        S.total_searches = before.total_searches + nq;
+        S.total_kernel_ms = before.total_kernel_ms + kms;
+        S.total_search_ms = before.total_search_ms + S.search_ms;
         return total;
     }
+    uint32_t retries = 0, launches = 0;
+    uint64_t ncand = 0;
     for (size_t i = 0; i < nq; i++) {
         test_configuration(queries[i]);
         SearchResult R;
         run_search(queries[i], algo == SSA_AMD_NW ? kAlgoNW : kAlgoSW, hitcount, bit_width, false, R);
         kms += stats().kernel_ms;
         cells += stats().cells;
+        retries += stats().part_retries;
+        ncand += stats().filter_candidates;
+        launches += stats().kernel_launches;
         const size_t n = std::min(hitcount, R.hits.size());
         for (size_t j = 0; j < n; j++) {
             const Hit& h = R.hits[j];
@@ -556,9 +566,14 @@ size_t ssa_amd_search_batch(const p_query* queries, size_t nq, int algo, size_t 
         if (counts) counts[i] = n;
         total += n;
     }
+    // batch aggregates, like the pipelined path (the running totals were
+    // advanced by run_search, once per query)
     ssa_amd_stats_t& S = stats();
     S.kernel_ms = kms;
     S.cells = cells;
+    S.part_retries = retries;
+    S.filter_candidates = ncand;
+    S.kernel_launches = launches;
     S.search_ms = now_ms() - t0;
     return total;
 }

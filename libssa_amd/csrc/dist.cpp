@@ -5,19 +5,20 @@
 // insertion log (ssa_amd_search(..., SSA_AMD_LOG)).  The reference merges its
 // worker threads' heaps on one host (manager.c:141-145); here the shards'
 // logs meet on rank 0 in ONE collective over xGMI: every rank contributes a
-// fixed slot of a count row plus kSlotRows (score, id, ...) rows, gathered by
-// ncclAllGather ((512 + 1) x 24 B = 12 KB per rank: latency-bound, one call).
-// Only when some log is longer than a slot (hitcount in the hundreds, or a
-// shard whose scores rise through its whole ID range) is a second, exact-size
-// ncclGather to rank 0 issued -- every rank knows whether it is needed from
-// the first round's counts, so the ranks never disagree on the collective
-// sequence.  Rank 0 then replays the logs in rank (= ID) order through the
-// reference heap: the 64-bit single-thread result, ties included.
+// fixed slot of a count row plus kSlotRows (score, id, ...) rows, gathered to
+// rank 0 by a single ncclGather ((512 + 1) x 24 B = 12 KB per rank,
+// latency-bound).  A log longer than its slot (hitcount in the hundreds, or a
+// shard whose scores rise through its whole ID range) sends the rest of its
+// rows point to point to rank 0 (ncclSend / ncclRecv): only that rank knows
+// its count before the gather and only rank 0 after it, so exactly those two
+// take part and every other rank's collective sequence is the one gather.
+// Rank 0 then replays the logs in rank (= ID) order through the reference
+// heap: the 64-bit single-thread result, ties included.
 //
 // The collectives go through a Transport: RCCL in production, and an
 // in-process one (ssa_amd_dist_init_fake: W host threads of one process
 // exchanging through shared memory) so that the slot addressing, the count
-// rows and the exact-size round run at W > 1 in the CPU tests too.
+// rows and the point-to-point remainder run at W > 1 in the CPU tests too.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
@@ -50,8 +51,11 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
-    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
@@ -70,11 +74,14 @@ const Rccl* rccl() {
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.comm_count = (decltype(r.comm_count))dlsym(h, "ncclCommCount");
-    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
     r.gather = (decltype(r.gather))dlsym(h, "ncclGather");
+    r.send = (decltype(r.send))dlsym(h, "ncclSend");
+    r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.comm_count || !r.all_gather || !r.gather ||
-        !r.error_string) {
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.comm_count || !r.gather || !r.send || !r.recv ||
+        !r.group_start || !r.group_end || !r.error_string) {
         print_error("RCCL lacks a required symbol");
         r = Rccl();
         return nullptr;
@@ -87,14 +94,18 @@ void nccl_check(ncclResult_t r, const char* what) {
 }
 
 // ---------------------------------------------------------------- transports
-// Host buffers in, host buffers out; every rank calls each collective in the
-// same order with the same byte count.
+// Host buffers in, host buffers out.  gather0 is collective (every rank, same
+// byte count); send0 / recv0 are point to point between one rank and rank 0,
+// called by exactly the two ranks involved.
 struct Transport {
     virtual ~Transport() = default;
-    // recv (every rank) gets rank r's `bytes` at recv + r * bytes
-    virtual void all_gather(const void* send, size_t bytes, uint8_t* recv) = 0;
     // rank 0's recv gets rank r's `bytes` at recv + r * bytes; recv unused elsewhere
     virtual void gather0(const void* send, size_t bytes, uint8_t* recv) = 0;
+    // this rank (not 0) sends `bytes` to rank 0
+    virtual void send0(const void* send, size_t bytes) = 0;
+    // rank 0 receives from[i].second bytes from rank from[i].first, in list
+    // order, concatenated into recv
+    virtual void recv0(const std::vector<std::pair<int, size_t>>& from, uint8_t* recv) = 0;
     virtual int ranks() = 0;      // ranks the communicator holds (ncclCommCount)
 };
 
@@ -104,42 +115,61 @@ struct RcclTransport final : Transport {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 0, device = -1;
     hipStream_t stream = nullptr;
-    size_t cap = 0;                       // bytes per rank of the buffers below
+    size_t send_cap = 0, recv_cap = 0, stage_cap = 0;
     uint8_t* d_send = nullptr;
-    uint8_t* d_recv = nullptr;            // world x cap
-    uint8_t* h_stage = nullptr;           // pinned, world x cap
+    uint8_t* d_recv = nullptr;
+    uint8_t* h_stage = nullptr;           // pinned
 
-    void reserve(size_t bytes) {
-        if (bytes <= cap) return;
+    void grow(uint8_t** p, size_t* cap, size_t bytes, bool pinned, const char* what) {
+        if (bytes <= *cap) return;
         (void)hipStreamSynchronize(stream);
-        (void)hipFree(d_send);
-        (void)hipFree(d_recv);
-        (void)hipHostFree(h_stage);
-        cap = bytes;
-        check(hipMalloc((void**)&d_send, cap), "gather send buffer");
-        check(hipMalloc((void**)&d_recv, cap * world), "gather receive buffer");
-        check(hipHostMalloc((void**)&h_stage, cap * world, hipHostMallocDefault), "pinned gather buffer");
+        if (pinned) (void)hipHostFree(*p);
+        else (void)hipFree(*p);
+        *p = nullptr;
+        *cap = std::max(bytes, 2 * *cap);
+        if (pinned) check(hipHostMalloc((void**)p, *cap, hipHostMallocDefault), what);
+        else check(hipMalloc((void**)p, *cap), what);
     }
-    void stage_in(const void* send, size_t bytes) {
+    void reserve(size_t send, size_t recv) {
+        grow(&d_send, &send_cap, send, false, "gather send buffer");
+        grow(&d_recv, &recv_cap, recv, false, "gather receive buffer");
+        grow(&h_stage, &stage_cap, std::max(send, recv), true, "pinned gather buffer");
+    }
+    void stage_in(const void* send, size_t bytes, size_t recv_bytes) {
         check(hipSetDevice(device), "hipSetDevice");
-        reserve(bytes);
+        reserve(bytes, recv_bytes);
         memcpy(h_stage, send, bytes);
         check(hipMemcpyAsync(d_send, h_stage, bytes, hipMemcpyHostToDevice, stream), "H2D log");
     }
-    void all_gather(const void* send, size_t bytes, uint8_t* recv) override {
-        stage_in(send, bytes);
-        nccl_check(rccl()->all_gather(d_send, d_recv, bytes, ncclUint8, comm, stream), "ncclAllGather");
-        check(hipMemcpyAsync(h_stage, d_recv, bytes * world, hipMemcpyDeviceToHost, stream), "D2H logs");
+    void stage_out(uint8_t* recv, size_t bytes) {
+        check(hipMemcpyAsync(h_stage, d_recv, bytes, hipMemcpyDeviceToHost, stream), "D2H logs");
         check(hipStreamSynchronize(stream), "gather");
-        memcpy(recv, h_stage, bytes * world);
+        memcpy(recv, h_stage, bytes);
     }
     void gather0(const void* send, size_t bytes, uint8_t* recv) override {
-        stage_in(send, bytes);
+        stage_in(send, bytes, rank == 0 ? bytes * world : 0);
         nccl_check(rccl()->gather(d_send, d_recv, bytes, ncclUint8, 0, comm, stream), "ncclGather");
-        if (rank == 0)
-            check(hipMemcpyAsync(h_stage, d_recv, bytes * world, hipMemcpyDeviceToHost, stream), "D2H logs");
-        check(hipStreamSynchronize(stream), "gather");
-        if (rank == 0) memcpy(recv, h_stage, bytes * world);
+        if (rank == 0) stage_out(recv, bytes * world);
+        else check(hipStreamSynchronize(stream), "gather");
+    }
+    void send0(const void* send, size_t bytes) override {
+        stage_in(send, bytes, 0);
+        nccl_check(rccl()->send(d_send, bytes, ncclUint8, 0, comm, stream), "ncclSend");
+        check(hipStreamSynchronize(stream), "send");
+    }
+    void recv0(const std::vector<std::pair<int, size_t>>& from, uint8_t* recv) override {
+        size_t total = 0;
+        for (const auto& f : from) total += f.second;
+        check(hipSetDevice(device), "hipSetDevice");
+        reserve(0, total);
+        nccl_check(rccl()->group_start(), "ncclGroupStart");
+        size_t at = 0;
+        for (const auto& f : from) {
+            nccl_check(rccl()->recv(d_recv + at, f.second, ncclUint8, f.first, comm, stream), "ncclRecv");
+            at += f.second;
+        }
+        nccl_check(rccl()->group_end(), "ncclGroupEnd");
+        stage_out(recv, total);
     }
     int ranks() override {
         int n = 0;
@@ -167,6 +197,9 @@ struct FakeGroup {
     int arrived = 0;
     uint64_t phase = 0;
     std::vector<const void*> send;
+    // point to point: rank r's pending message to rank 0 (nullptr: none)
+    std::vector<const void*> p2p;
+    std::vector<size_t> p2p_bytes;
 
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -195,8 +228,27 @@ struct FakeTransport final : Transport {
             for (int r = 0; r < g->world; r++) memcpy(recv + (size_t)r * bytes, g->send[r], bytes);
         g->barrier();
     }
-    void all_gather(const void* send, size_t bytes, uint8_t* recv) override { exchange(send, bytes, recv, true); }
     void gather0(const void* send, size_t bytes, uint8_t* recv) override { exchange(send, bytes, recv, false); }
+    void send0(const void* send, size_t bytes) override {
+        std::unique_lock<std::mutex> lk(g->mu);
+        g->p2p[rank] = send;
+        g->p2p_bytes[rank] = bytes;
+        g->cv.notify_all();
+        g->cv.wait(lk, [&] { return g->p2p[rank] == nullptr; });      // rank 0 has copied it
+    }
+    void recv0(const std::vector<std::pair<int, size_t>>& from, uint8_t* recv) override {
+        std::unique_lock<std::mutex> lk(g->mu);
+        for (const auto& f : from) {
+            g->cv.wait(lk, [&] { return g->p2p[f.first] != nullptr; });
+            if (g->p2p_bytes[f.first] != f.second)
+                fatal("fake transport: rank %d sent %zu bytes, rank 0 expected %zu", f.first, g->p2p_bytes[f.first],
+                      f.second);
+            memcpy(recv, g->p2p[f.first], f.second);
+            recv += f.second;
+            g->p2p[f.first] = nullptr;
+            g->cv.notify_all();
+        }
+    }
     int ranks() override { return g->world; }
     ~FakeTransport() override {
         std::lock_guard<std::mutex> lk(g_fake_mu);
@@ -207,8 +259,8 @@ struct FakeTransport final : Transport {
 struct DistState {
     std::unique_ptr<Transport> t;
     int rank = 0, world = 0;
-    std::vector<uint8_t> slots;           // world slots of round 1
-    std::vector<uint8_t> big_send, big_recv;
+    std::vector<uint8_t> slots;           // rank 0: the world slots of the gather
+    std::vector<uint8_t> rest;            // rank 0: the rows beyond the slots, received point to point
 };
 
 // the process's communicator (one per process, as RCCL's one rank per GPU)
@@ -221,6 +273,22 @@ thread_local DistState* t_fake = nullptr;
 
 DistState& cur() { return t_fake ? *t_fake : proc_state(); }
 
+// the last gather's time and rounds: the process's stats for the RCCL rank;
+// per thread for a fake rank (its W threads gather concurrently), laid over
+// the process's stats by ssa_amd_get_stats on that thread
+thread_local double t_gather_ms = 0;
+thread_local uint32_t t_gather_rounds = 0;
+
+void record_gather(double ms, uint32_t rounds) {
+    if (t_fake) {
+        t_gather_ms = ms;
+        t_gather_rounds = rounds;
+    } else {
+        stats().gather_ms = ms;
+        stats().gather_rounds = rounds;
+    }
+}
+
 Hit to_hit(const ssa_hit_t& x) { return Hit{x.score, x.db_id, x.query_id, x.db_strand, x.db_frame}; }
 
 void init_state(DistState& S, std::unique_ptr<Transport> t, int rank, int world) {
@@ -231,6 +299,13 @@ void init_state(DistState& S, std::unique_ptr<Transport> t, int rank, int world)
 }
 
 }  // namespace
+
+void dist_overlay_stats(ssa_amd_stats_t* out) {
+    if (!t_fake) return;
+    out->gather_ms = t_gather_ms;
+    out->gather_rounds = t_gather_rounds;
+}
+
 }  // namespace ssa
 
 using namespace ssa;
@@ -281,7 +356,7 @@ int ssa_amd_dist_init(int rank, int world, const void* id) {
     t->world = world;
     t->device = dev;
     check(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking), "hipStreamCreate");
-    t->reserve(slot_bytes());
+    t->reserve(slot_bytes(), rank == 0 ? slot_bytes() * (size_t)world : 0);
     init_state(S, std::move(t), rank, world);
     return 0;
 }
@@ -303,6 +378,8 @@ int ssa_amd_dist_init_fake(int rank, int world, int group) {
             g = std::make_shared<FakeGroup>();
             g->world = world;
             g->send.assign(world, nullptr);
+            g->p2p.assign(world, nullptr);
+            g->p2p_bytes.assign(world, 0);
         }
         if (g->world != world) {
             print_error("ssa_amd_dist_init_fake: group %d has world %d, not %d", group, g->world, world);
@@ -377,33 +454,66 @@ int ssa_amd_shard_bounds(const uint64_t* lengths, size_t n, size_t world, size_t
 size_t ssa_amd_gather_logs(const ssa_hit_t* log, size_t n, size_t hitcount, ssa_hit_t* out) {
     DistState& S = cur();
     if (!S.t) fatal("ssa_amd_gather_logs: ssa_amd_dist_init was not called");
+    const double t0 = now_ms();
     const size_t W = (size_t)S.world;
-    // round 1: every rank's slot -- a count row, then up to kSlotRows rows
+    // the one collective: every rank's slot -- a count row, then up to
+    // kSlotRows rows -- gathered to rank 0
     std::vector<uint8_t> mine(slot_bytes(), 0);
     const uint64_t cnt = n;
     memcpy(mine.data(), &cnt, 8);
     if (n) memcpy(mine.data() + kRow, log, std::min(n, kSlotRows) * kRow);
-    S.t->all_gather(mine.data(), slot_bytes(), S.slots.data());
+    S.t->gather0(mine.data(), slot_bytes(), S.rank == 0 ? S.slots.data() : nullptr);
+    uint32_t rounds = 1;
+    if (S.rank != 0) {
+        // a log longer than the slot: its remaining rows, point to point
+        if (n > kSlotRows) {
+            S.t->send0(log + kSlotRows, (n - kSlotRows) * kRow);
+            rounds = 2;
+        }
+        record_gather(now_ms() - t0, rounds);
+        return 0;
+    }
     std::vector<size_t> counts(W);
-    size_t longest = 0;
+    std::vector<std::pair<int, size_t>> from;
     for (size_t r = 0; r < W; r++) {
         uint64_t c;
         memcpy(&c, S.slots.data() + r * slot_bytes(), 8);
         counts[r] = c;
-        longest = std::max<size_t>(longest, c);
+        if (r > 0 && c > kSlotRows) from.emplace_back((int)r, (c - kSlotRows) * kRow);
     }
-    if (longest <= kSlotRows) {
-        if (S.rank != 0) return 0;
-        return ssa_amd_merge_logs((const ssa_hit_t*)(S.slots.data() + kRow), counts.data(), W, slot_bytes() / kRow,
-                                  hitcount, out);
+    size_t rest = 0;
+    for (const auto& f : from) rest += f.second;
+    S.rest.resize(std::max<size_t>(rest, 1));
+    if (!from.empty()) {
+        S.t->recv0(from, S.rest.data());
+        rounds = 2;
     }
-    // round 2 (every rank saw the same counts): exact-size gather to rank 0
-    S.big_send.assign(longest * kRow, 0);
-    if (n) memcpy(S.big_send.data(), log, n * kRow);
-    if (S.rank == 0) S.big_recv.resize(longest * kRow * W);
-    S.t->gather0(S.big_send.data(), longest * kRow, S.rank == 0 ? S.big_recv.data() : nullptr);
-    if (S.rank != 0) return 0;
-    return ssa_amd_merge_logs((const ssa_hit_t*)S.big_recv.data(), counts.data(), W, longest, hitcount, out);
+    // replay rank by rank, in rank (= ID) order: the slot rows, then the rest
+    // (rank 0's own log is local)
+    TopK heap(hitcount);
+    auto offer = [&](const ssa_hit_t* L, size_t c) {
+        for (size_t i = 0; i < c; i++) {
+            if (heap.full() && L[i].score <= heap.root_score()) continue;
+            heap.add(to_hit(L[i]));
+        }
+    };
+    const uint8_t* rp = S.rest.data();
+    for (size_t r = 0; r < W; r++) {
+        if (r == 0) {
+            offer(log, n);
+            continue;
+        }
+        offer((const ssa_hit_t*)(S.slots.data() + r * slot_bytes() + kRow), std::min(counts[r], kSlotRows));
+        if (counts[r] > kSlotRows) {
+            offer((const ssa_hit_t*)rp, counts[r] - kSlotRows);
+            rp += (counts[r] - kSlotRows) * kRow;
+        }
+    }
+    const std::vector<Hit> v = heap.sorted();
+    for (size_t i = 0; i < v.size(); i++)
+        out[i] = ssa_hit_t{v[i].score, v[i].id, v[i].qid, v[i].strand, v[i].frame, {0, 0, 0, 0, 0}};
+    record_gather(now_ms() - t0, rounds);
+    return v.size();
 }
 
 }  // extern "C"

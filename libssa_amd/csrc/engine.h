@@ -206,6 +206,7 @@ constexpr size_t kMaxBatchPipe = 16;    // queries per pipelined sub-batch (one 
 static_assert(kMaxBatchPipe == (size_t)kMaxFuse, "a sub-batch fuses into one pair_kernel launch");
 
 ssa_amd_stats_t& stats();
+void dist_overlay_stats(ssa_amd_stats_t* out);   // dist.cpp
 void check(hipError_t e, const char* what);
 double now_ms();
 

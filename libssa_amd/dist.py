@@ -1,17 +1,20 @@
-"""The one cross-GPU exchange of a sharded search.
+"""The one cross-GPU exchange of a sharded search, over
+torch.distributed -- the fallback beside the library's own RCCL gather
+(ssa_amd_gather_logs, csrc/dist.cpp), with the same shape.
 
 Each rank holds the insertion log of its ID shard (ssa_amd_search(...,
 SSA_AMD_LOG)); rank 0 gathers the logs in rank (= ID) order with a single
-torch.distributed all_gather of fixed-size buffers -- RCCL over xGMI on the GPU box ("nccl" backend),
-gloo in the CPU tests -- and replays them with ssa_amd_replay, which yields
-the reference's 64-bit single-thread top-k bit for bit.
+gather of fixed-size slots to rank 0 -- RCCL over xGMI on the GPU box ("nccl"
+backend), gloo in the CPU tests -- and replays them with ssa_amd_replay, which
+yields the reference's 64-bit single-thread top-k bit for bit.  A log longer
+than its slot sends the rest of its rows to rank 0 point to point.
 """
 from __future__ import annotations
 
 
 # rows per rank of the single fixed-size exchange; a shard log is a few
 # dozen to a few hundred entries (k * (1 + ln(shard / k)) expected), longer
-# ones take the two-step variable-size path
+# ones send their remainder point to point
 LOG_CAP = 512
 
 
@@ -23,37 +26,35 @@ def gather_logs(log, dist, rank: int, world: int, device, cap: int = LOG_CAP):
     """Gathers per-rank logs [(score, id, qid, strand, frame), ...] to rank 0.
     Returns the concatenation in rank order on rank 0, None elsewhere.
 
-    One all_gather of a fixed [cap + 1, 5] int64 buffer per rank (row 0 holds
-    the log length) -- a single RCCL collective per search.  If any rank's
-    log exceeds cap, every rank sees it in the headers and they fall back to
-    an exact-size gather."""
+    One gather of a fixed [cap + 1, 5] int64 slot per rank to rank 0 (row 0
+    holds the log length) -- a single collective per search.  A rank whose log
+    exceeds cap sends the remaining rows to rank 0 (dist.send), which knows
+    from the slot headers whom to receive from (dist.recv); no other rank
+    takes part."""
     import torch
     rows = _rows(log)
     n = len(rows)
     buf = torch.zeros((cap + 1, 5), dtype=torch.int64, device=device)
     buf[0, 0] = n
-    if 0 < n <= cap:
-        buf[1:n + 1] = torch.tensor(rows, dtype=torch.int64, device=device)
-    bufs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf)
-    lens = torch.stack([b[0, 0] for b in bufs]).tolist()
-    if max(lens) <= cap:
-        if rank != 0:
-            return None
-        parts = [bufs[r][1:lens[r] + 1] for r in range(world) if lens[r] > 0]
-        return [tuple(x) for x in torch.cat(parts).tolist()] if parts else []
-    # rare: some log is longer than cap -- gather exact sizes
-    mx = max(lens)
-    pad = torch.zeros((mx, 5), dtype=torch.int64, device=device)
     if n:
-        pad[:n] = torch.tensor(rows, dtype=torch.int64, device=device)
-    out = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
-    dist.gather(pad, out, dst=0)
+        buf[1:min(n, cap) + 1] = torch.tensor(rows[:cap], dtype=torch.int64, device=device)
+    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, bufs, dst=0)
     if rank != 0:
+        if n > cap:
+            dist.send(torch.tensor(rows[cap:], dtype=torch.int64, device=device), dst=0)
         return None
+    lens = [int(b[0, 0]) for b in bufs]
     merged = []
     for r in range(world):
-        merged += [tuple(x) for x in out[r][: lens[r]].tolist()]
+        if r == 0:
+            merged += [tuple(x) for x in rows]
+            continue
+        merged += [tuple(x) for x in bufs[r][1:min(lens[r], cap) + 1].tolist()]
+        if lens[r] > cap:
+            rest = torch.empty((lens[r] - cap, 5), dtype=torch.int64, device=device)
+            dist.recv(rest, src=r)
+            merged += [tuple(x) for x in rest.tolist()]
     return merged
 
 

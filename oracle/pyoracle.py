@@ -224,7 +224,7 @@ MODE_SEARCH8_AVX2 = 7
 
 def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_open: int = 0,
             gap_extend: int = 0, k: int = 10, chunk: int = 1000, threads: int = 1, repeat: int = 1,
-            db_off=None, views=None, chunk_counts=False, raw_hits=False):
+            db_off=None, views=None, chunk_counts=False, raw_hits=False, times=False):
     """Runs the reference harness.  Returns raw per-seq scores (mode 0), the
     tables blob (mode 4), or (hits, overflow_count, nseq, seconds) for the
     searches -- overflow_count is the 16-bit count, or (o8, o16) for the
@@ -232,7 +232,8 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
     array is appended.  views: a list of equal-length query views (searched
     as one multi-view query) instead of `query`.  raw_hits: the hits as an
     int64 [count, 2] (score, id) array instead of a list of tuples (the
-    multi-million-hit full-size fixtures)."""
+    multi-million-hit full-size fixtures).  times: the searches return
+    the seconds of every repeat (a list) in place of the best."""
     nviews = 0
     if views is not None:
         nviews = len(views)
@@ -298,6 +299,10 @@ def ref_run(mode: int, algo: int = 0, query=None, seqs=None, matrix=None, gap_op
     o8, nch = struct.unpack_from("<QQ", data, pos + 24)
     if mode == MODE_SEARCH8_AVX2:
         ovf = (o8, ovf)
+    if times:
+        tpos = pos + 40 + 16 * nch
+        nrep = struct.unpack_from("<Q", data, tpos)[0]
+        secs = list(struct.unpack_from(f"<{nrep}d", data, tpos + 8))
     if chunk_counts:
         per = np.frombuffer(data, dtype=np.uint64, count=2 * nch, offset=pos + 40).reshape(nch, 2).copy()
         return hits, ovf, ns, secs, per

@@ -32,7 +32,7 @@
  * Search modes (1, 2, 3, 7) answer: u64 count, (i64 score, u64 id) x count,
  * u64 16-bit overflows, u64 non-empty sequences, f64 best seconds, u64
  * 8-bit overflows, u64 nchunks, (u64 o8, u64 o16) per chunk (with chunk = 1:
- * per-sequence overflow flags).
+ * per-sequence overflow flags), u64 repeats, f64 seconds of every repeat.
  * The header's pad field is the number of query views (0 or 1: one); the
  * query blob then holds that many views of qlen / views residues each
  * (e.g. both strands of a nucleotide query, searcher.c:42-90).
@@ -199,9 +199,11 @@ static void run_search(FILE* out) {
     tres_t* res = (tres_t*)calloc(T, sizeof(tres_t));
     pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
     double best = 1e30;
+    const uint32_t nrep = R.repeat ? R.repeat : 1;
+    double* times = (double*)calloc(nrep, sizeof(double));
     p_minheap merged = NULL;
     size_t ovf = 0, ovf8 = 0;
-    for (uint32_t rep = 0; rep < (R.repeat ? R.repeat : 1); rep++) {
+    for (uint32_t rep = 0; rep < nrep; rep++) {
         if (merged) minheap_exit(merged);
         for (int t = 0; t < T; t++) if (res[t].heap) { minheap_exit(res[t].heap); res[t].heap = NULL; }
         NEXT_CHUNK = 0;
@@ -218,6 +220,7 @@ static void run_search(FILE* out) {
         }
         minheap_sort(merged);
         double dt = now() - t0;
+        times[rep] = dt;
         if (dt < best) best = dt;
     }
     uint64_t cnt = merged->count;
@@ -237,6 +240,10 @@ static void run_search(FILE* out) {
     fwrite(&o8, 8, 1, out);
     fwrite(&nch, 8, 1, out);
     fwrite(CH_OVF, 8, 2 * NCHUNKS, out);
+    uint64_t nr = nrep;
+    fwrite(&nr, 8, 1, out);
+    fwrite(times, 8, nrep, out);
+    free(times);
 }
 
 static void run_scores(FILE* out) {

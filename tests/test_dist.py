@@ -125,6 +125,7 @@ def _fake_gather(logs, k, group):
     import libssa_amd as S
     W = len(logs)
     res, ranks, errs = [None] * W, [None] * W, []
+    rounds = [None] * W
 
     def run(r):
         try:
@@ -132,6 +133,7 @@ def _fake_gather(logs, k, group):
             try:
                 ranks[r] = S.dist_ranks()
                 res[r] = S.gather_logs(logs[r], k)
+                rounds[r] = S.stats()["gather_rounds"]
             finally:
                 S.dist_finalize()
         except Exception as e:  # pragma: no cover - reported below
@@ -144,6 +146,11 @@ def _fake_gather(logs, k, group):
         t.join(60)
     assert not any(t.is_alive() for t in th), "fake collective did not drain"
     assert not errs, errs
+    # one slot gather on every rank; the point-to-point remainder only on the
+    # ranks whose log exceeds the 512-row slot and on rank 0 when any does
+    long = [len(x) > 512 for x in logs]
+    assert rounds[1:] == [2 if x else 1 for x in long[1:]], rounds
+    assert rounds[0] == (2 if any(long[1:]) else 1), rounds
     return res, ranks
 
 
@@ -160,10 +167,10 @@ def _cuts(n, W, rng, empty):
 def test_native_gather_fake_world(W, k, kind):
     """ssa_amd_gather_logs at W > 1 without hardware: W threads exchange
     through the library's in-process transport (the same slot layout, count
-    rows and exact-size second round as over RCCL).  Rank 0 gets the
+    rows and point-to-point remainder as over RCCL).  Rank 0 gets the
     single-process reference top-k (tie IDs included), the others nothing.
     "rising" scores make every shard log longer than the 512-row slot at
-    k = 300, i.e. the ncclGather round; "empty" leaves ranks with no log."""
+    k = 300, i.e. the point-to-point remainder; "empty" leaves ranks with no log."""
     rng = np.random.default_rng(W * 1000 + k)
     n = 6000
     if kind == "rising":
@@ -361,3 +368,55 @@ def test_bench_launcher_refuses_more_ranks_than_gpus():
     r = _bench(["--gpus", "2", "--no-cpu-baseline"], env_extra={"SSA_DIST_BACKEND": "nccl"})
     assert r.returncode == 2
     assert "GPU(s) visible" in r.stderr
+
+
+def _split_worker(rank, world, port, outdir):
+    """One rank of the N > 1 bench line's per-rank split (bench.rank_split):
+    synthetic per-rank times, the real all-gather over gloo."""
+    import argparse
+    import json
+    import sys
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(BENCH))
+    import bench
+    job = bench.Job(rank, world, dist, "cpu", "gloo")
+    # rank r: kernel (10 + r) ms over (1 + r / 10) x 1e9 residues of a 400-residue query
+    res = int((1 + rank / 10) * 1e9)
+    sh = argparse.Namespace(residues=res, cells_local=float(res) * 400, seqs=1000 + rank)
+    avg = {"kernel_ms": 10.0 + rank, "search_ms": 10.2 + rank}
+    split = {"search_s": [(10.2 + rank) / 1e3] * 5, "gather_s": [(0.05 + 0.01 * rank) / 1e3] * 4 + [1e-3]}
+    out = bench.rank_split(job, sh, avg, split, (10.5 + world) / 1e3)
+    if rank == 0:
+        with open(os.path.join(outdir, "split.json"), "w") as f:
+            json.dump(out, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_rank_split_explains_the_step(tmp_path, world):
+    """The N > 1 bench line explains its own result (what the driver's first
+    8-GPU run reports): per-rank kernel and search ms (min / max / rank of
+    max), the gather's own time (median and max over ranks and steps), the
+    kernel balance efficiency, the residue imbalance of the cut and the step
+    split, all gathered from every rank over the process group."""
+    import json
+    mp.spawn(_split_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    d = json.load(open(tmp_path / "split.json"))
+    assert d["kernel_ms"] == [10.0 + r for r in range(world)]
+    assert d["search_ms"] == [round(10.2 + r, 4) for r in range(world)]
+    assert d["kernel_ms_max"] == 10.0 + world - 1 and d["kernel_ms_argmax"] == world - 1
+    assert d["search_ms_min"] == 10.2 and d["search_ms_argmax"] == world - 1
+    assert d["gather_ms"]["max"] == 1.0
+    assert d["gather_ms_median"] == [round(0.05 + 0.01 * r, 4) for r in range(world)]
+    assert d["seqs"] == [1000 + r for r in range(world)]
+    res = np.array([(1 + r / 10) * 1e9 for r in range(world)])
+    kms = np.array([10.0 + r for r in range(world)])
+    eff = (res * 400).sum() / (kms.max() * 1e-3) / ((res * 400) / (kms * 1e-3)).sum()
+    assert abs(d["kernel_balance_efficiency"] - eff) < 1e-4 and d["kernel_balance_efficiency"] < 1
+    assert abs(d["residue_imbalance"] - res.max() / res.mean()) < 1e-5
+    sp = d["step_split_ms"]
+    assert sp["kernel_max"] == kms.max() and abs(sp["search_host_overhead"] - 0.2) < 1e-6
+    assert abs(sp["step"] - (sp["search_host_overhead"] + sp["kernel_max"] + sp["gather_median"] + sp["rest"])) < 1e-3
