@@ -81,6 +81,8 @@ void DeviceDB::release() {
     if (h_cnt) (void)hipHostFree(h_cnt);
     d_flags = nullptr; d_flist = nullptr; d_cnt = nullptr; h_cnt = nullptr;
     flags_cap = 0;
+    cnt_dirty = true;                     // a new d_cnt block starts unzeroed
+    gate_count = 0;
     d_lscratch = nullptr;
     lscratch_cap = 0;
     d_upblk = nullptr;
@@ -1071,7 +1073,18 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     // counters and the long-entry dispatch gate start at 0
     uint32_t* const gate = (uint32_t*)(D.d_cnt + 2 * kMaxBatchPipe);
     uint32_t gate_total = 0, gate_base = 0;   // long workgroups launched in all views / before this view
-    if (E > 0) check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe + 16, D.stream), "memset");
+    // (no per-search memset: the gate word only grows, see DeviceDB::gate_count;
+    // the counters are zeroed only when this search computes them)
+    if (E > 0) {
+        if (D.cnt_dirty) {
+            check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe + 16, D.stream), "memset");
+            D.gate_count = 0;
+            D.cnt_dirty = false;
+        } else if (want_counts) {
+            check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe, D.stream), "memset");
+        }
+    }
+    const uint32_t gate0 = D.gate_count;
     // single query view and a small k: only heap-changing candidates come back
     const double t_prep0 = now_ms();
     double prep = 0, sync_wait = 0;
@@ -1632,6 +1645,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 la.seq0 = 0;
                 la.nseq = long4 * 64;
                 gate_total += la.nseq;                         // one workgroup per entry
+                D.gate_count += la.nseq;
                 check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
                 check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
                 check(hipEventRecord(D.ev[7], D.stream_long), "event");
@@ -1640,6 +1654,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 la.seq0 = long4 * 64;
                 la.nseq = (long_groups - long4) * 64;
                 gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
+                D.gate_count += (la.nseq + kLongWaves - 1) / kLongWaves;
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
@@ -1694,7 +1709,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const uint32_t resident = (uint32_t)std::max<size_t>(1, kPairLdsMax / std::max<size_t>(lds_long, 1)) *
                                           (D.nsimd / 4);
                 ta.gate = gate;
-                ta.gate_target = std::min<uint32_t>(gate_total, gate_base + std::min<uint32_t>(512, resident));
+                ta.gate_target = gate0 + std::min<uint32_t>(gate_total, gate_base + std::min<uint32_t>(512, resident));
             }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {
@@ -2072,7 +2087,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             } else {
                 perr = out.sparse ? D.h_fbuf[2] : *h_perr;
             }
-            if (perr) return false;
+            if (perr) {
+                D.cnt_dirty = true;          // (the wait-timeout word is cleared before the re-run)
+                return false;
+            }
         }
         const double t_post0 = now_ms();
 

@@ -99,6 +99,13 @@ struct DeviceDB {
     uint32_t* d_part = nullptr;
     size_t part_cap = 0;
     uint32_t part_epoch = 0;              // the last pair launch's handoff flag value (StripArgs::part_epoch)
+    // the long-entry dispatch gate (d_cnt's gate word) is never cleared per
+    // search: it counts every long workgroup launched since d_cnt was last
+    // zeroed, and the tables kernel waits for this search's share above
+    // gate_count.  cnt_dirty: zero the whole block before the next search
+    // (fresh memory, or a strip part's wait-timeout word was raised)
+    uint32_t gate_count = 0;
+    bool cnt_dirty = true;
     uint32_t* d_smax = nullptr;
     size_t smax_cap = 0;
     uint4* d_rowbuf2 = nullptr;           // part 1's row buffer (StripArgs::rowbuf2), as d_rowbuf

@@ -689,7 +689,8 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
         // at ~20 ms of the 100 MHz real-time counter, so a gate that is never
         // reached only costs time, never a hang
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.gate_target &&
+        // (the gate word only grows across searches: a wrap-safe comparison)
+        while ((int32_t)(__hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - a.gate_target) < 0 &&
                __builtin_amdgcn_s_memrealtime() - t0 < 2000000ull)
             __builtin_amdgcn_s_sleep(8);
     }

@@ -1526,6 +1526,43 @@ def test_fullsize_matches_reference_hash(name, tmp_path):
     S.free_sequence(qq)
 
 
+REF64 = json.load(open(os.path.join(GOLDEN, "ref64.json")))
+
+
+@pytest.mark.parametrize("name", sorted(REF64))
+def test_tie_band_matches_reference_search64(name, tmp_path):
+    """The tie band at scale, pinned by the reference's OWN 64-bit search:
+    tests/golden/ref64.json holds the top-64 of the reference's one-thread
+    search_64 (src/algo/64/search_64.c:44-79 -> minheap_add,
+    src/util/minheap.c:50-91; tools/gen_golden.py ref64) on tie-heavy DBs --
+    the 28-symbol SW and NW fixtures, the 25-symbol one and the first 100 k
+    reads of C5's DB (q = 10 000 nt) -- whose 64th score lies inside a band
+    of equal scores.  sw_align / nw_align's top-64 (score and ID) equals that
+    list, at API widths 16 and 8."""
+    c = REF64[name]
+    q, codes, off = _fullsize_inputs(c)
+    assert len(off) - 1 == c["nonempty"] and int(off[-1]) == c["residues"]
+    dna = c["kind"] == "dna"
+    if c["matrix"].startswith("const"):
+        a, b = c["matrix"][5:].split("_")
+        spec = ("const", int(a), int(b))
+    else:
+        spec = ("builtin", c["matrix"])
+    configure(dna, spec, c["gap_open"], c["gap_extend"])
+    path = os.path.join(str(tmp_path), "db.fas")
+    syn.write_fasta(path, codes, off, dna)
+    del codes
+    S.init_db(path)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q, nucleotide=dna))
+    fn = S.sw_align if c["algo"] == "sw" else S.nw_align
+    top = c["top64"]
+    assert top[-1][0] == top[-2][0], "the fixture's 64th score is inside a tie band"
+    for width in (16, 8):
+        got = [[h["score"], h["id"]] for h in fn(qq, 64, width)]
+        assert got == top, (width, [x for x in zip(got, top) if x[0] != x[1]][:5])
+    S.free_sequence(qq)
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", [k for k in LARGE if k in FULL])
 def test_large_db_matches_reference(name, tmp_path):

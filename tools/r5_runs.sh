@@ -1,0 +1,66 @@
+#!/bin/bash
+# Round-5 GPU runs, one function per run (the command lines the round-5
+# profiles and DESIGN.md cite).  Usage, on the GPU box from the repo root:
+#   bash tools/r5_runs.sh <name> [args]
+# Every GPU step runs under its own timeout; a failing step ends the function.
+set -o pipefail
+
+r5_tests() (
+    # the GPU parity suite (optionally -k filter as $1)
+    mkdir -p gpurun_out/r5
+    K=${1:+-k "$1"}
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread $K \
+        > gpurun_out/r5/gpu_tests.log 2>&1 || { tail -40 gpurun_out/r5/gpu_tests.log; exit 1; }
+    tail -3 gpurun_out/r5/gpu_tests.log
+)
+
+r5_bench() (
+    # the default bench line (C2 + north_star + cpu_baseline)
+    mkdir -p gpurun_out/r5
+    timeout -k 10 600 python bench.py > gpurun_out/r5/default.json 2> gpurun_out/r5/default.err \
+        || { tail -30 gpurun_out/r5/default.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/r5/default.json')); c=d.get('cpu_baseline',{}); print(d['value'], d['kernel']['kernel_gcups'], d.get('topk_vs_reference'), d['north_star']['value'], d['north_star'].get('topk_vs_reference'), c.get('value'), c.get('one_thread_gcups'))"
+)
+
+r5_rehearse() (
+    # gloo rehearsals of the N > 1 line: 2 and 4 ranks on the one GPU
+    mkdir -p gpurun_out/r5
+    for n in 2 4; do
+        SSA_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus $n --no-cpu-baseline \
+            > gpurun_out/r5/gloo$n.json 2> gpurun_out/r5/gloo$n.err || { tail -30 gpurun_out/r5/gloo$n.err; exit 1; }
+        python -c "import json; d=json.load(open('gpurun_out/r5/gloo$n.json')); print($n, d['value'], d.get('rehearsal'), d.get('topk_vs_reference'), json.dumps(d.get('ranks_split',{}).get('step_split_ms')), d['north_star'].get('topk_vs_reference'), json.dumps(d['north_star'].get('ranks_split',{}).get('step_split_ms')))"
+    done
+)
+
+r5_pmc_shapes() (
+    # valu / lds / stats PMC passes for C2, the reference's benchmark shape
+    # with its own scoring (BLOSUM50 -3/-1) and with BLOSUM62 -11/-1, and the
+    # Swiss-Prot form: effective clock, VALU per cell, LDS conflicts
+    for cfg in "c2:--config c2" "ref:--config ref" "ref_b62:--config ref --matrix blosum62 --gap-open -11 --gap-extend -1" "sprot:--config sprot"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        PASSES="stats valu lds" bash tools/profile_pmc.sh gpurun_out/r5/pmc/$name $args || exit 1
+        echo "$name done"
+    done
+)
+
+r5_medians() (
+    # 5 x 20 steps of C2, ref, sprot (kernel and end-to-end TCUPS)
+    mkdir -p gpurun_out/r5/medians
+    for i in 1 2 3 4 5; do
+        for cfg in c2 ref sprot; do
+            timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-north-star --no-cpu-baseline \
+                > gpurun_out/r5/medians/${cfg}_$i.json 2> gpurun_out/r5/medians/${cfg}_$i.err || { tail -20 gpurun_out/r5/medians/${cfg}_$i.err; exit 1; }
+        done
+    done
+    python - <<'EOF'
+import json, glob, statistics as st
+for cfg in ("c2", "ref", "sprot"):
+    v, k = [], []
+    for f in sorted(glob.glob(f"gpurun_out/r5/medians/{cfg}_*.json")):
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+        v.append(d["value"]); k.append(d["kernel"]["kernel_gcups"])
+    print(cfg, "median end-to-end", st.median(v), "kernel", st.median(k), v)
+EOF
+)
+
+"r5_$@"
