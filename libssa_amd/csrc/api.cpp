@@ -438,6 +438,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "counters")) cfg().counters = (int)value;
     else if (!strcmp(name, "part_wait_us")) cfg().part_wait_us = std::max(0L, value);
     else if (!strcmp(name, "rescore32")) cfg().rescore32 = (int)value;
+    else if (!strcmp(name, "filter_host")) cfg().filter_host = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -53,6 +53,9 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
+    int filter_host = 1;                  // 1: the top-k filter writes its result into pinned host memory and
+                                          // the host spins on its sequence word (no D2H copy, no stream
+                                          // synchronisation); 0: copy + hipStreamSynchronize
 };
 Config& cfg();
 // whether a search computes the overflow counters (Config::counters)

@@ -1106,6 +1106,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     if (ind && !(out.sparse && V > 1 && V <= kMaxBatchPipe)) fatal("device_search: batch not pipelinable");
     const bool multi = out.sparse && V > 1 && !ind;
     const bool piped = multi || ind;
+    // the sparse single-pass filter hands its result straight to the host
+    // (FilterArgs::host_out) unless something else still has to be copied
+    // back on the stream (the overflow counters)
+    const bool host_direct = C.filter_host && out.sparse && !ind && !want_counts;
     // every lane fits a view's overflow list (reference: no limit on the
     // sequences search_16.c:101-109 re-runs at 64 bits)
     const size_t ovf_capv = std::max<size_t>((size_t)D.ngroups * 64, 1);
@@ -2055,11 +2059,23 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             f.counters = D.d_fbuf;
             f.status = gate + 2;
             f.cand = (uint2*)(D.d_fbuf + kFilterHeader);
+            if (host_direct) {
+                // the filter writes header + first candidates into h_fbuf and
+                // then the sequence word the host spins on below
+                if (++D.filter_seq == 0) D.filter_seq = 1;
+                __atomic_store_n(&D.h_fbuf[kFilterSeqWord], 0u, __ATOMIC_RELEASE);
+                f.host_out = D.h_fbuf;
+                f.host_cap = (uint32_t)std::min<size_t>(D.h_cand_cap, f.n);
+                f.host_seq = D.filter_seq;
+                f.done = gate + 3;
+            }
             check(launch_filter(f, st), "filter launch");
-            // one copy: counters (incl. the overflow counts) + the first candidates
-            const size_t first = std::min<size_t>(D.h_cand_cap, f.n);
-            check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
-                  "D2H candidates");
+            if (!host_direct) {
+                // one copy: counters (incl. the overflow counts) + the first candidates
+                const size_t first = std::min<size_t>(D.h_cand_cap, f.n);
+                check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
+                      "D2H candidates");
+            }
         } else {
             check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
             // (the first kOvfPinned entries; d_ovf holds ovf_capv + 1 dwords)
@@ -2073,9 +2089,30 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         const bool perr_in_header = ind || out.sparse;
         if (parts_used && !perr_in_header)
             check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
-        check(hipEventRecord(D.ev[3], st), "event");
         const double t_sync0 = now_ms();
-        check(hipStreamSynchronize(st), "search");
+        if (host_direct) {
+            // spin on the filter's sequence word in pinned memory: the result is
+            // here as soon as the last filter block has written it, before the
+            // kernel's end-of-dispatch cache writeback and completion signal
+            // (the stream keeps that tail; the next search queues behind it).
+            // A drained stream without the word is a library bug: fatal.
+            const volatile uint32_t* seqw = D.h_fbuf + kFilterSeqWord;
+            for (uint64_t it = 1; __atomic_load_n(seqw, __ATOMIC_ACQUIRE) != D.filter_seq; it++) {
+                if ((it & 1023) == 0) {
+                    const hipError_t q = hipStreamQuery(st);
+                    if (q == hipSuccess) {
+                        if (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) != D.filter_seq)
+                            fatal("device filter result did not reach the host");
+                        break;
+                    }
+                    if (q != hipErrorNotReady) check(q, "search");
+                }
+                __builtin_ia32_pause();
+            }
+        } else {
+            check(hipEventRecord(D.ev[3], st), "event");
+            check(hipStreamSynchronize(st), "search");
+        }
         sync_wait += now_ms() - t_sync0;
         // a strip part gave up waiting for its group's first part: this
         // launch's scores are incomplete -- the caller runs the search again
@@ -2206,8 +2243,12 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         }
         check(hipEventElapsedTime(&t, ev_k1, D.ev[2]), "elapsed");
         wms += t;
-        check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
-        dms += t;
+        if (!host_direct) {
+            // (the direct path has no copy: the filter's own time is in the
+            // kernel trace, d2h_ms stays 0)
+            check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
+            dms += t;
+        }
         if (counted && !ind) {
             out.dev_o8 = D.h_cnt[0];
             out.dev_o16 = D.h_cnt[1];

@@ -197,7 +197,18 @@ struct FilterArgs {
     // slice of the scratch arrays.  nq 0/1: one.
     uint32_t nq;
     size_t q_scores, q_ovf, q_counters;
+    // single pass (nq <= 1): the result straight into pinned host memory
+    // instead of a D2H copy -- the last filter_select block to finish (done:
+    // a device word, 0 between searches, reset by that block) writes header
+    // words 0..14 and the first host_cap candidates to host_out, then
+    // host_seq into host_out[kFilterSeqWord] at system scope (the host spins
+    // on that word).  host_out null: none.
+    uint32_t* host_out;
+    uint32_t host_cap;
+    uint32_t host_seq;
+    uint32_t* done;
 };
+constexpr int kFilterSeqWord = 15;    // header word that carries FilterArgs::host_seq
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
 
 

@@ -654,12 +654,36 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
     if (e < a.nviews) a.counters[3 + e] = a.ovf_count[(size_t)e * a.ovf_stride];
     if (e == 0 && a.status) a.counters[2] = *a.status;
-    if (e >= a.n) return;
-    const int32_t x = a.scores[a.order ? a.order[e] : e];
-    const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
-    if (x == INT32_MIN || x > t) {
-        const uint32_t i = atomicAdd(&a.counters[0], 1u);
-        a.cand[i] = make_uint2(e, (uint32_t)x);
+    if (e < a.n) {
+        const int32_t x = a.scores[a.order ? a.order[e] : e];
+        const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
+        if (x == INT32_MIN || x > t) {
+            const uint32_t i = atomicAdd(&a.counters[0], 1u);
+            a.cand[i] = make_uint2(e, (uint32_t)x);
+        }
+    }
+    if (!a.host_out) return;
+    // the last block to finish copies the result to the host (FilterArgs::host_out)
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();                       // this block's candidates, device-wide
+        last = atomicAdd(a.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();                           // every block's candidates visible here
+    const uint32_t nc = __hip_atomic_load(&a.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < kFilterSeqWord)
+        a.host_out[threadIdx.x] = threadIdx.x == 0 ? nc : __hip_atomic_load(&a.counters[threadIdx.x], __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_AGENT);
+    uint2* hc = (uint2*)(a.host_out + kFilterHeader);
+    for (uint32_t i = threadIdx.x; i < min(nc, a.host_cap); i += 256) hc[i] = a.cand[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *a.done = 0;                           // (the next search's pass counts from 0 again)
+        __threadfence_system();                // the copies reach host memory before the sequence word
+        __hip_atomic_store(a.host_out + kFilterSeqWord, a.host_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -668,6 +692,7 @@ hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     const uint32_t nq = a.nq > 1 ? a.nq : 1u;
     hipLaunchKernelGGL(filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
     hipLaunchKernelGGL(filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+    if (a.host_out && (nq > 1 || !a.done)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256, nq), dim3(256), 0, st, a);
     return hipGetLastError();
 }

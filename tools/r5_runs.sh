@@ -63,4 +63,29 @@ for cfg in ("c2", "ref", "sprot"):
 EOF
 )
 
+r5_ab() (
+    # alternating A/B of bench options on one box: $1 = name, $2 = config,
+    # $3 = option string A, $4 = option string B, $5 = repeats (default 3)
+    mkdir -p gpurun_out/r5/ab/$1
+    for i in $(seq 1 ${5:-3}); do
+        for v in A B; do
+            if [ $v = A ]; then o="$3"; else o="$4"; fi
+            timeout -k 10 300 python bench.py --config $2 --steps 20 --warmup 3 --no-north-star --no-cpu-baseline $o \
+                > gpurun_out/r5/ab/$1/${v}_$i.json 2> gpurun_out/r5/ab/$1/${v}_$i.err || { tail -20 gpurun_out/r5/ab/$1/${v}_$i.err; exit 1; }
+            python -c "import json; d=json.loads(open('gpurun_out/r5/ab/$1/${v}_$i.json').read().strip().splitlines()[-1]); print('$1 $v$i', d['value'], d['kernel']['kernel_gcups'], d['ms_per_step'], d['kernel']['avg_ms'], d['host_ms']['search_call'], d['host_ms']['sync_wait'], d.get('topk_vs_reference'))"
+        done
+    done
+)
+
+r5_clock() (
+    # valu passes alternating between two configurations (effective clock)
+    for i in 1 2; do
+        for cfg in "ref:--config ref" "ref_b62:--config ref --matrix blosum62 --gap-open -11 --gap-extend -1"; do
+            name=${cfg%%:*}; args=${cfg#*:}
+            PASSES="valu" bash tools/profile_pmc.sh gpurun_out/r5/clock/${name}_$i $args || exit 1
+            cp gpurun_out/r5/clock/${name}_$i/valu.log gpurun_out/r5/clock/${name}_$i/stats.log 2>/dev/null
+        done
+    done
+)
+
 "r5_$@"
