@@ -53,9 +53,11 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
-    int filter_host = 1;                  // 1: the top-k filter writes its result into pinned host memory and
+    int filter_host = 0;                  // 1/2: the top-k filter writes its result into pinned host memory and
                                           // the host spins on its sequence word (no D2H copy, no stream
-                                          // synchronisation); 0: copy + hipStreamSynchronize
+                                          // synchronisation; 1 with a system-scope release, 2 with system-
+                                          // scope stores and a store-completion wait); 0 (default: 1 measured
+                                          // no gain, profiles/r05/ab/filter_host): copy + hipStreamSynchronize
 };
 Config& cfg();
 // whether a search computes the overflow counters (Config::counters)

@@ -746,21 +746,21 @@ static constexpr uint32_t kLongMaxGroups = 256;
 // same box, alternating runs).
 static int pair_strip_np(int opt, bool nw, uint32_t prow, size_t m) {
     if (opt == 16 || opt == 24 || opt == 32 || opt == 40 || (opt == 36 && !nw)) return opt;
-    auto tbl = [&](int np) { return (size_t)prow * prow * (np + 4) * 4; };
+    auto tbl = [&](int np) { return (size_t)pair_lds_rows(prow - 1) * (np + 4) * 4; };
     if (!nw) {
         // short SW queries whose rows fill 32-row strips better than 48-row
         // ones run at four waves per SIMD when four tables fit a CU
         // (profiles/r02/short_query_np.txt: q = 30 +1.4 %, q = 64 +2.1 %;
         // q = 100 is 5 % faster at 48 rows)
         const bool short_q = m <= 32 || (m > 48 && m <= 64);
-        return short_q && 4 * tbl(16) <= kPairLdsMax ? 16 : 24;
+        return short_q && pair_wgs_per_cu(tbl(16)) >= 4 ? 16 : 24;
     }
     // an NW query of at most 48 rows runs only the capture strip: at three
     // waves per SIMD rather than the 80-row strips' two (q = 30: +4.8 %,
     // profiles/r02/short_query_np.txt)
     if (m <= 48) return 24;
     for (int np : {40, 32})
-        if (2 * tbl(np) <= kPairLdsMax) return np;
+        if (pair_wgs_per_cu(tbl(np)) >= 2) return np;
     return 24;
 }
 
@@ -912,8 +912,8 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     // alphabet of a codes
     auto pair_wgs = [&](size_t a) {
         const int pn = pair_strip_np(C.pair_np, nw, (uint32_t)a + 1, m);
-        const size_t b = (a + 1) * (a + 1) * (pn + 4) * 4;
-        const size_t w = b > kPairLdsMax ? (size_t)0 : std::min<size_t>(pn <= 24 ? 3 : 2, kPairLdsMax / b);
+        const size_t b = (size_t)pair_lds_rows((uint32_t)a) * (pn + 4) * 4;
+        const size_t w = std::min<size_t>(pn <= 24 ? 3 : 2, pair_wgs_per_cu(b));
         return std::make_pair(w, pn);
     };
     bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
@@ -951,7 +951,7 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     const uint32_t prow = A + 1;
     // pair kernel main strip height: 2 * pair_np rows (16 -> 32 rows, 24 -> 48)
     const int pnp = pair_strip_np(C.pair_np, nw, prow, m);
-    const size_t pair_lds = (size_t)prow * prow * (pnp + 4) * 4;
+    const size_t pair_lds = (size_t)pair_lds_rows(A) * (pnp + 4) * 4;
     // pair kernel (diagonal-relative f16 patterns): only when no more than
     // a handful of entries exceed its length bound (those are re-scored
     // by the int64 kernel); otherwise the strip kernels
@@ -1322,7 +1322,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             dres = D.d_res_cls;
         }
-        const uint32_t A = vp.A, prow = vp.prow;
+        const uint32_t A = vp.A;
         const int64_t minM = vp.minM, maxM = vp.maxM;
         const uint32_t nmax16 = vp.nmax16, nw_base = vp.nw_base, long_groups = vp.long_groups;
         const int pnp = vp.pnp;
@@ -1710,7 +1710,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 // reached only as early ones retire, and the wait would run
                 // into its 20 ms bound; and at most 512, the rest follow the
                 // first in order)
-                const uint32_t resident = (uint32_t)std::max<size_t>(1, kPairLdsMax / std::max<size_t>(lds_long, 1)) *
+                const uint32_t resident = (uint32_t)std::max<size_t>(1, pair_wgs_per_cu(lds_long)) *
                                           (D.nsimd / 4);
                 ta.gate = gate;
                 ta.gate_target = gate0 + std::min<uint32_t>(gate_total, gate_base + std::min<uint32_t>(512, resident));
@@ -1870,7 +1870,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             // 0's start: the host prepared the other views in between)
             if (fused && v + 1 == V) check(hipEventRecord(D.vev[2 * V], st), "event");
             if (!fused || v + 1 == V)
-                check(launch_pair(b, pnp, tail_np, nw, (size_t)prow * prow * (lnp + 4) * 4, st), "pair kernel launch");
+                check(launch_pair(b, pnp, tail_np, nw, (size_t)pair_lds_rows(A) * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
@@ -2068,6 +2068,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.host_cap = (uint32_t)std::min<size_t>(D.h_cand_cap, f.n);
                 f.host_seq = D.filter_seq;
                 f.done = gate + 3;
+                f.host_fence = C.filter_host == 1 ? 1u : 0u;
             }
             check(launch_filter(f, st), "filter launch");
             if (!host_direct) {

@@ -8,7 +8,26 @@ namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup
 constexpr int kPairWaves = 4;      // waves per pair_kernel workgroup (they share one pair table)
-constexpr size_t kPairLdsMax = 160 * 1024;  // pair table budget: one workgroup per CU (49 KiB for 20-letter proteins: 3)
+constexpr size_t kPairLdsMax = 160 * 1024;  // pair table budget: one workgroup per CU (47 KiB for 20-letter proteins: 3)
+
+// The pair kernel's LDS table holds the residue pairs (current c1, previous
+// c0) a column after column 0 can meet: c0 a real code (c1 any, padding
+// included) and (pad, pad) -- a padding column is followed only by padding,
+// and (c1, pad) with c1 real occurs only at column 0, whose operand the
+// kernel reads from the global table instead.  (A + 1) A + 1 rows for A real
+// codes instead of (A + 1)^2: 421 for 20 letters, 463 for 21.
+__host__ __device__ constexpr uint32_t pair_lds_rows(uint32_t A) { return (A + 1) * A + 1; }
+__host__ __device__ constexpr uint32_t pair_lds_row(uint32_t A, uint32_t c1, uint32_t c0) {
+    return c0 < A ? c1 * A + c0 : (A + 1) * A;
+}
+// Workgroups of `bytes` dynamic LDS that one gfx950 CU keeps resident (LDS
+// alone): allocations are rounded up to 1 280 B (measured, tools/ubench/
+// lds_occ.hip, profiles/r05/lds_occ.txt: 40 960 B -> 4, 53 760 B -> 3,
+// 54 208 B -> 2, 75 776 B -> 2 -- 160 KiB / 3 = 54 613 B is not reachable)
+constexpr size_t kLdsGranule = 1280;
+constexpr size_t pair_wgs_per_cu(size_t bytes) {
+    return bytes == 0 ? 4 : kPairLdsMax / ((bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule);
+}
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
 constexpr int kMaxFuse = 16;       // queries one pair_kernel launch may score (StripArgs::nq)
@@ -207,6 +226,9 @@ struct FilterArgs {
     uint32_t host_cap;
     uint32_t host_seq;
     uint32_t* done;
+    uint32_t host_fence;       // 1: system-scope release before the sequence word (an L2 writeback);
+                               // 0: system-scope relaxed stores, each thread waits for its own
+                               // stores' completion before the block's barrier and the sequence word
 };
 constexpr int kFilterSeqWord = 15;    // header word that carries FilterArgs::host_seq
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

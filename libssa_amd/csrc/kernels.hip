@@ -674,16 +674,29 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     if (!last) return;
     __threadfence();                           // every block's candidates visible here
     const uint32_t nc = __hip_atomic_load(&a.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto put = [&](uint32_t* p, uint32_t v) {
+        if (a.host_fence) *p = v;
+        else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
     if (threadIdx.x < kFilterSeqWord)
-        a.host_out[threadIdx.x] = threadIdx.x == 0 ? nc : __hip_atomic_load(&a.counters[threadIdx.x], __ATOMIC_RELAXED,
-                                                                              __HIP_MEMORY_SCOPE_AGENT);
-    uint2* hc = (uint2*)(a.host_out + kFilterHeader);
-    for (uint32_t i = threadIdx.x; i < min(nc, a.host_cap); i += 256) hc[i] = a.cand[i];
+        put(a.host_out + threadIdx.x,
+            threadIdx.x == 0 ? nc : __hip_atomic_load(&a.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    uint32_t* hc = a.host_out + kFilterHeader;
+    for (uint32_t i = threadIdx.x; i < min(nc, a.host_cap); i += 256) {
+        const uint2 c = a.cand[i];
+        put(hc + 2 * i, c.x);
+        put(hc + 2 * i + 1, c.y);
+    }
+    if (!a.host_fence) __builtin_amdgcn_s_waitcnt(0);   // this thread's stores are complete
     __syncthreads();
     if (threadIdx.x == 0) {
         *a.done = 0;                           // (the next search's pass counts from 0 again)
-        __threadfence_system();                // the copies reach host memory before the sequence word
-        __hip_atomic_store(a.host_out + kFilterSeqWord, a.host_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.host_fence) {
+            __threadfence_system();            // the copies reach host memory before the sequence word
+            __hip_atomic_store(a.host_out + kFilterSeqWord, a.host_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            __hip_atomic_store(a.host_out + kFilterSeqWord, a.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -794,7 +807,6 @@ __global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
     const GroupDesc gd = a.groups[g];
     const uint32_t nblk = (gd.ncols + 15) >> 4;
     const uint32_t pad = a.prow - 1;
-    const uint32_t pairB = a.prow * a.row_bytes;
     uint4 cur = nblk ? a.res[(size_t)gd.blk * 64 + lane] : make_uint4(0, 0, 0, 0);
     for (uint32_t b = 0; b < nblk; b++) {
         const uint4 nxt = b + 1 < nblk ? a.res[(size_t)(gd.blk + b + 1) * 64 + lane] : make_uint4(pad, 0, 0, 0);
@@ -806,7 +818,9 @@ __global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
             const uint32_t dn = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xffu;
             // past the group's last column: the padding code
             const uint32_t dnx = b * 16 + k + 1 < gd.ncols ? dn : pad;
-            o[k] = (dnx * pairB + d * a.row_bytes) >> 4;      // 16-byte units: < 2^16 for any table in LDS
+            // LDS row of the pair (dnx, d): kernels.h pair_lds_row (d is the
+            // padding code only inside the padding, where dnx is too)
+            o[k] = (pair_lds_row(pad, dnx, d) * a.row_bytes) >> 4;   // 16-byte units: < 2^16 for any table in LDS
         }
         uint4* dst = a.out + (size_t)(gd.blk + b) * 128 + lane;
 #pragma unroll

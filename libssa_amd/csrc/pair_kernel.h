@@ -29,8 +29,10 @@ namespace ssa {
 // low half for the current residue, high half for the previous one (the
 // skew).  Indexing the LDS table by the residue pair (d_j, d_{j-1}) returns
 // it directly -- no v_bfi_b32 per cell and no VGPR copy of the previous row.
-// The table has (alpha+1)^2 rows of NP dwords (alpha = compact DB alphabet,
-// +1 for padding): 441 rows / 35 KiB for a 20-letter DB.  It is shared by
+// The table has (alpha+1)^2 rows of NP dwords in global memory (alpha =
+// compact DB alphabet, +1 for padding); LDS holds the (alpha+1)alpha+1 of
+// them a column after column 0 can meet (kernels.h pair_lds_row): 421 rows /
+// 46 KiB at stride NP+4 for a 20-letter DB.  It is shared by
 // the workgroup's waves, so they step through the strips together (one
 // barrier per strip; groups of a workgroup are adjacent in the length order,
 // so their strips take nearly the same time).
@@ -237,13 +239,18 @@ pair_kernel(const StripArgs a) {
         constexpr int NPS = decltype(np_c)::value;
         constexpr bool CAPS = decltype(cap_c)::value;
         const uint32_t ROWW = NPS == NP || a.nstrips > 0 ? NP + 4 : NPS + 4;
-        // ---- the whole workgroup stages this strip's pair table
+        // ---- the whole workgroup stages this strip's pair table: the rows a
+        // column after column 0 can meet (kernels.h pair_lds_row), from the
+        // global table's (A+1)^2 rows (row c1 * prow + c0)
         __syncthreads();
-        const uint32_t ntab4 = prow * prow * (NPS / 4);
+        const uint32_t A_ = a.alpha;
+        const uint32_t ntab4 = pair_lds_rows(A_) * (NPS / 4);
         const uint4* src = (const uint4*)tab;
         for (uint32_t i = threadIdx.x; i < ntab4; i += 64 * W) {
-            const uint32_t row = i / (NPS / 4), k = i % (NPS / 4);
-            *(uint4*)(lds + row * ROWW + 4 * k) = src[i];
+            const uint32_t lrow = i / (NPS / 4), k = i % (NPS / 4);
+            const uint32_t c1 = lrow < (A_ + 1) * A_ ? lrow / A_ : A_;
+            const uint32_t c0 = lrow < (A_ + 1) * A_ ? lrow - c1 * A_ : A_;
+            *(uint4*)(lds + lrow * ROWW + 4 * k) = src[(c1 * prow + c0) * (NPS / 4) + k];
         }
         __syncthreads();
         if (!active) return;
@@ -347,9 +354,10 @@ pair_kernel(const StripArgs a) {
         // the SW accumulators A)
         uint32_t P[NPS];
         {
-            const uint32_t rowB = ROWW * 4;
+            // column 0's pair (d_0, pad) is not in LDS (pair_lds_row): the
+            // global table's row, from L2, once per strip
             const uint32_t d0 = resp[0].x & 0xffu;
-            load_row<NPS>(P, (const uint32_t*)((const char*)lds + (d0 * prow + a.alpha) * rowB));
+            load_row<NPS>(P, tab + (size_t)(d0 * prow + a.alpha) * NPS);
         }
 
         for (uint32_t b = 0; b < nblk; b++) {

@@ -1035,10 +1035,19 @@ def test_device_filter_candidate_count_is_exact(n, pattern):
         S.init_db(_write_db(tmp, codes, off))
         qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
         ids = np.arange(n, dtype=np.uint64)
-        for k in (1, 10, 64):
-            got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
-            assert got == po.topk(exp, ids, k), (pattern, k)
-            assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k)
+        try:
+            # option filter_host: the result written into pinned host memory
+            # by the last filter block (with a system-scope release, or with
+            # system-scope stores) instead of the D2H copy -- incl. more
+            # candidates than the pinned buffer holds ("rising")
+            for fh in (0, 1, 2):
+                S.set_option("filter_host", fh)
+                for k in (1, 10, 64):
+                    got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+                    assert got == po.topk(exp, ids, k), (pattern, k, fh)
+                    assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, fh)
+        finally:
+            S.set_option("filter_host", 0)
         S.free_sequence(qq)
 
 
