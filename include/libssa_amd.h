@@ -74,6 +74,10 @@ typedef struct {
                                 collective, rank 0's replay) */
     uint32_t gather_rounds;  /* 1: the slot gather alone; 2: this rank also sent (or rank 0 received)
                                 log rows beyond the 512-row slot point to point */
+    uint32_t rare_merged;    /* DB residue codes the last search scored through one upper-bound class
+                                (option "rare_merge"; 0: none) */
+    uint32_t rare_rescored;  /* entries holding one of them that the device filter forwarded and the
+                                int32 tier re-scored exactly */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -125,6 +129,13 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "part_wait_us" N     bound of a strip part's wait for its group's first part (default
  *                        2000000); a timed-out wait makes the search run again without parts
  *                        (stats part_retries), results unchanged
+ *   "rare_merge" 1|0     1 (default): when a query's residue classes leave the pair table too big
+ *                        for three workgroups per CU, the rarest classes share one class scoring
+ *                        the maximum of their rows, and the entries holding them that the device
+ *                        filter forwards are re-scored exactly (stats rare_merged / rare_rescored)
+ *   "filter_host" 0|1|2  the device filter's result through a D2H copy (0, default) or written by
+ *                        the filter into pinned host memory (1: system-scope release, 2: system-
+ *                        scope stores), the host spinning on a sequence word
  *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
  *                        m_run's INFO line): -1 (default) only at output mode
  *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always

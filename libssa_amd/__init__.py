@@ -69,7 +69,8 @@ class ssa_amd_stats_t(Structure):
                 ("sync_wait_ms", c_double), ("strip_rows", c_uint32), ("counters", c_uint32),
                 ("long_entries", c_uint32), ("long_kernel", ctypes.c_char * 24), ("part_retries", c_uint32),
                 ("total_searches", c_uint64), ("total_kernel_ms", c_double), ("total_search_ms", c_double),
-                ("filter_candidates", c_uint64), ("gather_ms", c_double), ("gather_rounds", c_uint32)]
+                ("filter_candidates", c_uint64), ("gather_ms", c_double), ("gather_rounds", c_uint32),
+                ("rare_merged", c_uint32), ("rare_rescored", c_uint32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -237,11 +238,10 @@ def save_db(path): return load().ssa_amd_save_db(_b(path))
 def load_db(path): return load().ssa_amd_load_db(_b(path))
 
 
-_stats_buf = ssa_amd_stats_t()
 
 
 def stats():
-    s = _stats_buf
+    s = ssa_amd_stats_t()          # (per call: threads of a fake dist group read their own)
     load().ssa_amd_get_stats(ctypes.byref(s))
     d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
     d["kernel"] = d["kernel"].decode()

@@ -115,7 +115,12 @@ void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPl
     S.long_entries = sc.empty() ? 0 : sc[0].long_entries;
     snprintf(S.long_kernel, sizeof S.long_kernel, "%s", sc.empty() ? "" : sc[0].long_kernel);
     S.part_retries = 0;
-    for (const SearchScores& x : sc) S.part_retries += x.part_retries;
+    S.rare_merged = S.rare_rescored = 0;
+    for (const SearchScores& x : sc) {
+        S.part_retries += x.part_retries;
+        S.rare_merged = std::max(S.rare_merged, x.rare_merged);
+        S.rare_rescored += x.rare_rescored;
+    }
 }
 
 void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResult& R) {
@@ -439,6 +444,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "part_wait_us")) cfg().part_wait_us = std::max(0L, value);
     else if (!strcmp(name, "rescore32")) cfg().rescore32 = (int)value;
     else if (!strcmp(name, "filter_host")) cfg().filter_host = (int)value;
+    else if (!strcmp(name, "rare_merge")) cfg().rare_merge = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -53,6 +53,9 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
+    int rare_merge = 1;                   // 1: when the query's residue classes leave the pair table too big for
+                                          // three workgroups per CU, the rarest classes share one upper-bound
+                                          // class and the forwarded entries holding them are re-scored exactly
     int filter_host = 0;                  // 1/2: the top-k filter writes its result into pinned host memory and
                                           // the host spins on its sequence word (no D2H copy, no stream
                                           // synchronisation; 1 with a system-scope release, 2 with system-

@@ -75,6 +75,14 @@ void DeviceDB::release() {
     timeline_cap = timeline_rows = 0;
     dfree(d_entry_lane);
     d_entry_lane = nullptr;
+    dfree(d_emask);
+    d_emask = nullptr;
+    code_entries.clear();
+    dfree(d_exact);
+    d_exact = nullptr;
+    exact_cap = 0;
+    if (h_exact) (void)hipHostFree(h_exact);
+    h_exact = nullptr;
     hmm_cap = 0;
     d_res_cls = nullptr;
     cls_key.clear();
@@ -116,7 +124,11 @@ void DeviceDB::release() {
 
 constexpr size_t kOvfPinned = 4096;      // overflow entries the pinned mirrors hold (more: pageable copies)
 // per-search device upload block: [kernel-code matrix 8 KiB][code-0 row 256 B][top boundary][query]
-constexpr size_t kUpHeader = 8192 + 256;
+// per-search upload block: kernel-code matrix (8 KB), code 0's row (256 B),
+// the compact-code matrix of the rare-code merge's exact re-score (8 KB)
+constexpr size_t kUpExactMat = 8192 + 256;
+constexpr size_t kUpHeader = 8192 + 256 + 8192;
+constexpr size_t kExactPinned = 1024;    // exact re-score results the pinned mirror holds
 
 // ------------------------------------------------------------ entry codes
 // Mapped residues of one entry, as db_adapter.c:47-110 builds them: NT codes
@@ -868,6 +880,12 @@ struct ViewPlan {
     uint32_t main_strips = 0;
     int tail_np = 0;
     size_t tail_off = 0, qpt_words = 0;   // pair tables: tail offset, total dwords
+    // rare-code merge: compact codes scored through the upper-bound class
+    // (bit c), an upper bound of the entries that hold one, the int32 tier's
+    // rows per lane for their exact re-score
+    uint32_t merge_mask = 0;
+    uint64_t merge_entries = 0;
+    int merge_rl = 0;
 };
 struct PlanForce {
     int64_t minM, maxM;
@@ -875,7 +893,8 @@ struct PlanForce {
     uint32_t long_scale;
 };
 
-static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, const PlanForce* force, ViewPlan& vp) {
+static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, const PlanForce* force, ViewPlan& vp,
+                      bool allow_merge = false) {
     const Config& C = cfg();
     const int Q = C.gap_open, R = C.gap_extend;
     const int64_t* M = matrix().m;
@@ -918,12 +937,79 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     };
     bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
                    pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
+    // Rare-code merge (Swiss-Prot's X, B, Z, U, O: ~0.04 % of the residues,
+    // in ~12 % of the entries): when the classes still leave the pair table
+    // too big for three workgroups per CU, the rarest classes share ONE class
+    // that scores the element-wise maximum of their rows.  An entry holding
+    // one of them then scores an upper bound of its true score (max-plus DP
+    // is monotone in the profile); the device filter leaves such entries out
+    // of its heap-root bounds and forwards every one whose bound could enter
+    // the heap to an exact re-score (the int32 tier over the compact codes),
+    // so the result is unchanged.  Only while those entries stay a small
+    // share (a quarter of the DB at most) and the tier is exact for them.
+    int ub = -1;
+    if (allow_merge && C.rare_merge && C.sw_kernel == 0 && np == 16 && !D.code_entries.empty() && m > 0) {
+        const size_t A0 = cls_rep.size();
+        int64_t xlo = INT64_MAX, xhi = INT64_MIN;        // the exact re-score's profile bounds
+        for (size_t i = 0; i < m; i++)
+            for (uint32_t c = 0; c < D.alpha; c++) {
+                const int64_t x = M[((size_t)D.code_of[c] << 5) + qv.seq[i]];
+                xlo = std::min(xlo, x);
+                xhi = std::max(xhi, x);
+            }
+        const int rlx = rescore32_rl(D, m, D.alpha, C.gap_open, C.gap_extend, xlo, xhi);
+        if (rlx > 0 && pair_wgs(A0).first < 3 && A0 >= 3) {
+            std::vector<uint64_t> ce(A0, 0);
+            for (uint32_t c = 0; c < D.alpha; c++) ce[cls_of[c]] += D.code_entries[c];
+            std::vector<uint32_t> ord(A0);
+            std::iota(ord.begin(), ord.end(), 0u);
+            std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return ce[x] < ce[y]; });
+            uint64_t fl = ce[ord[0]];
+            for (size_t k = 2; k < A0; k++) {
+                fl += ce[ord[k - 1]];
+                if (fl * 4 > D.meta.size()) break;
+                if (pair_wgs(A0 - k + 1).first < 3) continue;
+                // classes ord[0..k) become one: the others keep their order,
+                // the merged class comes last
+                std::vector<uint8_t> merged(A0, 0), idx(A0, 0);
+                for (size_t i = 0; i < k; i++) merged[ord[i]] = 1;
+                std::vector<uint8_t> rep2;
+                for (size_t j = 0; j < A0; j++)
+                    if (!merged[j]) {
+                        idx[j] = (uint8_t)rep2.size();
+                        rep2.push_back(cls_rep[j]);
+                    }
+                ub = (int)rep2.size();
+                for (size_t j = 0; j < A0; j++)
+                    if (merged[j]) idx[j] = (uint8_t)ub;
+                for (uint32_t c = 0; c < D.alpha; c++) {
+                    if (merged[cls_of[c]]) vp.merge_mask |= 1u << c;
+                    cls_of[c] = idx[cls_of[c]];
+                }
+                rep2.push_back(0);               // (the merged class has no representative row)
+                cls_rep = std::move(rep2);
+                vp.merge_entries = fl;
+                vp.merge_rl = rlx;
+                use_cls = true;
+                break;
+            }
+        }
+    }
     // kernel codes: the classes, or the compact codes themselves
     uint32_t A = use_cls ? (uint32_t)cls_rep.size() : D.alpha;
     std::vector<int64_t>& crow = vp.crow;
     crow.assign((size_t)std::max<uint32_t>(A, 1) * 32, -1);
     for (uint32_t c = 0; c < A; c++)
-        memcpy(&crow[(size_t)c * 32], M + ((size_t)(use_cls ? cls_rep[c] : D.code_of[c]) << 5), 32 * 8);
+        if ((int)c != ub) memcpy(&crow[(size_t)c * 32], M + ((size_t)(use_cls ? cls_rep[c] : D.code_of[c]) << 5), 32 * 8);
+    if (ub >= 0) {
+        // the upper-bound class: the maximum of its members' rows
+        for (int y = 0; y < 32; y++) {
+            int64_t mx = INT64_MIN;
+            for (uint32_t c = 0; c < D.alpha; c++)
+                if ((vp.merge_mask >> c) & 1) mx = std::max(mx, M[((size_t)D.code_of[c] << 5) + y]);
+            crow[(size_t)ub * 32 + y] = mx;
+        }
+    }
     vp.use_cls = use_cls;
     // profile bounds over the kernel codes
     int64_t minM = INT64_MAX, maxM = INT64_MIN;
@@ -1027,6 +1113,28 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     vp.qpt_words = qpt_words;
 }
 
+// per entry the compact codes it holds and per code the entries holding it
+// (the rare-code merge's decision and flags), once per packed DB
+static void ensure_entry_masks(DeviceDB& D) {
+    if (!D.code_entries.empty()) return;
+    const size_t E = D.meta.size();
+    check(hipMalloc((void**)&D.d_emask, std::max<size_t>(E, 1) * 4), "entry code masks");
+    EntryMaskArgs a{};
+    a.res = D.d_res;
+    a.groups = D.d_groups;
+    a.lane_out = D.d_lane_out;
+    a.ngroups = D.ngroups;
+    a.pad = D.alpha;
+    a.out = D.d_emask;
+    check(launch_entry_mask(a, D.stream), "entry mask launch");
+    std::vector<uint32_t> h(E);
+    check(hipMemcpyAsync(h.data(), D.d_emask, E * 4, hipMemcpyDeviceToHost, D.stream), "D2H entry masks");
+    check(hipStreamSynchronize(D.stream), "entry masks");
+    D.code_entries.assign(std::max<uint32_t>(D.alpha, 1), 0);
+    for (uint32_t x : h)
+        for (; x; x &= x - 1) D.code_entries[__builtin_ctz(x)]++;
+}
+
 bool batch_pipelinable(size_t nqueries, size_t k) {
     return nqueries > 1 && k > 0 && k <= (size_t)kFilterMaxK && !cfg().no_filter;
 }
@@ -1109,7 +1217,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     // the sparse single-pass filter hands its result straight to the host
     // (FilterArgs::host_out) unless something else still has to be copied
     // back on the stream (the overflow counters)
-    const bool host_direct = C.filter_host && out.sparse && !ind && !want_counts;
+    bool host_direct = C.filter_host && out.sparse && !ind && !want_counts;
+    // the rare-code merge (plan_view) needs the single-pass filter and no
+    // counters (they decide from exact scores)
+    const bool allow_merge = C.rare_merge && V == 1 && !ind && out.sparse && !want_counts && E > 0;
+    if (allow_merge && D.alpha > 21) ensure_entry_masks(D);
     // every lane fits a view's overflow list (reference: no limit on the
     // sequences search_16.c:101-109 re-runs at 64 bits)
     const size_t ovf_capv = std::max<size_t>((size_t)D.ngroups * 64, 1);
@@ -1301,8 +1413,20 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // planned every query up front with shared bounds
         ViewPlan vpl;
         if (fused) vpl = fplans[v];
-        else plan_view(D, qv, nw, np, nullptr, vpl);
+        else plan_view(D, qv, nw, np, nullptr, vpl, allow_merge);
         const ViewPlan& vp = vpl;
+        const bool merge = vp.merge_mask != 0;
+        if (merge) {
+            host_direct = false;           // (the exact re-score follows the filter)
+            // lanes, then int64 scores, for every entry that holds a merged code
+            const size_t cap = std::max<uint64_t>(vp.merge_entries, 1);
+            if (D.exact_cap < cap) {
+                dfree(D.d_exact);
+                check(hipMalloc((void**)&D.d_exact, cap * 12 + 16), "exact re-score list");
+                D.exact_cap = cap;
+            }
+            if (!D.h_exact) check(hipHostMalloc((void**)&D.h_exact, kExactPinned * 12, hipHostMallocDefault), "pinned");
+        }
         const bool use_cls = vp.use_cls;
         const std::vector<uint8_t>& cls_of = vp.cls_of;
         const uint4* dres = D.d_res;
@@ -1450,6 +1574,13 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         uint8_t* up_q = hup + ((blk_bytes + 15) & ~(size_t)15);
         memcpy(up_m, Mc, 1024 * 8);
         for (int y = 0; y < 32; y++) memcpy(up_m + 8192 + 8 * y, &M[y], 8);   // code 0's row, M[0][y]
+        if (merge) {
+            // the compact codes' matrix: the exact re-score of merged-code entries
+            int64_t* mx = (int64_t*)(up_m + kUpExactMat);
+            for (int x = 0; x < 32; x++)
+                for (int y = 0; y < 32; y++)
+                    mx[(x << 5) + y] = (uint32_t)x < D.alpha ? M[((size_t)D.code_of[x] << 5) + y] : -1;
+        }
         if (!top.empty()) memcpy(up_t, top.data(), top.size() * 4);
         memcpy(up_s, qv.seq, m);
         if (fused && v == 0)
@@ -2070,7 +2201,51 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.done = gate + 3;
                 f.host_fence = C.filter_host == 1 ? 1u : 0u;
             }
+            const size_t xcap_al = (D.exact_cap + 1) & ~(size_t)1;     // (int64 scores 8-byte aligned)
+            if (merge) {
+                f.emask = D.d_emask;
+                f.merge_mask = vp.merge_mask;
+                f.entry_lane = (const uint2*)D.d_entry_lane;
+                f.exact_lanes = D.d_exact;
+            }
             check(launch_filter(f, st), "filter launch");
+            if (merge) {
+                // the forwarded merged-code entries, exactly: the int32 tier
+                // over their lanes (count: the filter header's word 1) on the
+                // compact-code residues and matrix
+                LongArgs xa{};
+                xa.res = D.d_res;
+                xa.groups = D.d_groups;
+                xa.lane_len = D.d_lane_len;
+                xa.lane_out = D.d_lane_out;
+                xa.query = D.d_query;
+                xa.matrix = (const int64_t*)(dup + kUpExactMat);
+                xa.m = (uint32_t)m;
+                xa.alpha = D.alpha;
+                xa.gap_open = Q;
+                xa.gap_extend = R;
+                xa.list = D.d_exact;
+                xa.list_count = D.d_fbuf + 1;
+                xa.list_out = (int64_t*)(D.d_exact + xcap_al);
+                xa.nseq = (uint32_t)D.exact_cap;
+                xa.blocks = (uint32_t)std::min<size_t>(kRescoreBlocks, (D.exact_cap + kLongWaves - 1) / kLongWaves);
+                if (m > (size_t)64 * vp.merge_rl) {
+                    xa.stride = D.group_ncols[0] + 16;
+                    const size_t need = (size_t)xa.blocks * kLongWaves * xa.stride;
+                    if (D.rscratch_cap < need) {
+                        check(hipStreamSynchronize(st), "sync");
+                        dfree(D.d_rscratch);
+                        check(hipMalloc((void**)&D.d_rscratch, need * 8), "re-score scratch");
+                        D.rscratch_cap = need;
+                    }
+                    xa.scratch = D.d_rscratch;
+                }
+                check(launch_long(xa, 1, vp.merge_rl, nw, st), "exact re-score launch");
+                const size_t nx = std::min(kExactPinned, D.exact_cap);
+                check(hipMemcpyAsync(D.h_exact, D.d_exact, nx * 4, hipMemcpyDeviceToHost, st), "D2H exact lanes");
+                check(hipMemcpyAsync(D.h_exact + kExactPinned * 4, D.d_exact + xcap_al, nx * 8, hipMemcpyDeviceToHost, st),
+                      "D2H exact scores");
+            }
             if (!host_direct) {
                 // one copy: counters (incl. the overflow counts) + the first candidates
                 const size_t first = std::min<size_t>(D.h_cand_cap, f.n);
@@ -2219,6 +2394,32 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
                 const uint32_t nov = D.h_fbuf[3 + vv];
                 if (nov) take_wide(multi ? vv : v, nov, out, multi ? vv : v);
+            }
+            if (merge) {
+                // exact scores of the forwarded merged-code entries (after the
+                // overflow re-score's, which scored them on the merged class)
+                const uint32_t nx = D.h_fbuf[1];
+                const uint32_t* xl = (const uint32_t*)D.h_exact;
+                const int64_t* xs = (const int64_t*)(D.h_exact + kExactPinned * 4);
+                std::vector<uint32_t> bl;
+                std::vector<int64_t> bs;
+                if (nx > kExactPinned) {
+                    const size_t xcap_al = (D.exact_cap + 1) & ~(size_t)1;
+                    bl.resize(nx);
+                    bs.resize(nx);
+                    check(hipMemcpy(bl.data(), D.d_exact, 4 * (size_t)nx, hipMemcpyDeviceToHost), "D2H exact lanes");
+                    check(hipMemcpy(bs.data(), D.d_exact + xcap_al, 8 * (size_t)nx, hipMemcpyDeviceToHost),
+                          "D2H exact scores");
+                    xl = bl.data();
+                    xs = bs.data();
+                }
+                for (uint32_t i = 0; i < nx; i++) {
+                    const uint32_t e = D.lane_out[xl[i]];
+                    out.wide[e] = xs[i];
+                    D.h_scores[e] = INT32_MIN;
+                }
+                out.rare_rescored = nx;
+                out.rare_merged = (uint32_t)__builtin_popcount(vp.merge_mask);
             }
         } else {
             take_wide(v, D.h_ovf[0], out, v);

@@ -92,6 +92,16 @@ struct DeviceDB {
     uint4* d_timeline = nullptr;          // option "timeline": [long lanes][pair groups] wave rows
     size_t timeline_cap = 0, timeline_rows = 0;
     uint32_t* d_entry_lane = nullptr;     // [entries] (length, lane) in entry order
+    // rare-code merge (engine.cpp plan_view): per entry the
+    // compact codes it holds, and per compact code the entries holding it
+    // (computed on first use; empty: not yet)
+    uint32_t* d_emask = nullptr;
+    std::vector<uint64_t> code_entries;
+    // the exact re-score of forwarded merged-code entries: lanes [exact_cap],
+    // then their int64 scores; pinned mirror of the first kExactPinned of each
+    uint32_t* d_exact = nullptr;
+    size_t exact_cap = 0;
+    uint8_t* h_exact = nullptr;
     size_t hmm_cap = 0;                   // lanes
     unsigned long long* d_cnt = nullptr;  // [kMaxBatchPipe][2]
     unsigned long long* h_cnt = nullptr;  // pinned mirror (+ 16 B: the gate block's error word)
@@ -194,6 +204,8 @@ struct SearchScores {
     char long_kernel[24] = {};           // which (ssa_amd_stats_t::long_kernel)
     uint32_t fused_views = 0;            // views one fused pair_kernel launch scored (0: not fused)
     uint32_t part_retries = 0;           // 1: a strip-part wait timed out, the search ran again without parts
+    uint32_t rare_merged = 0;            // compact codes scored through one upper-bound class (0: none)
+    uint32_t rare_rescored = 0;          // forwarded merged-code entries re-scored exactly
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;

@@ -229,6 +229,16 @@ struct FilterArgs {
     uint32_t host_fence;       // 1: system-scope release before the sequence word (an L2 writeback);
                                // 0: system-scope relaxed stores, each thread waits for its own
                                // stores' completion before the block's barrier and the sequence word
+    // rare-code merge (single pass, identity order): an entry whose codes
+    // (emask[e]) meet merge_mask holds an UPPER BOUND of its score (the
+    // merged class scores the maximum of its members).  It is left out of
+    // the maxima like an overflowed entry; when forwarded, its lane
+    // (entry_lane[e].y) is appended to exact_lanes (count: counters[1]) for
+    // the exact re-score.  emask null: none.
+    const uint32_t* emask;
+    uint32_t merge_mask;
+    const uint2* entry_lane;
+    uint32_t* exact_lanes;
 };
 constexpr int kFilterSeqWord = 15;    // header word that carries FilterArgs::host_seq
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);
@@ -340,6 +350,19 @@ struct PairAddrArgs {
     uint32_t row_bytes;        // table row stride: (NP + 4) * 4, or (NPT + 4) * 4 without main strips
 };
 hipError_t launch_pair_addr(const PairAddrArgs& a, hipStream_t st);
+
+// Per DB entry, the set of compact residue codes it holds (bit c: code c
+// occurs), from the packed residue blocks: one wave per group, one lane per
+// entry (engine.cpp: the rare-code merge's flags).
+struct EntryMaskArgs {
+    const uint4* res;          // residue blocks, compact codes
+    const GroupDesc* groups;
+    const uint32_t* lane_out;  // lane -> entry (0xffffffff: padding lane)
+    uint32_t ngroups;
+    uint32_t pad;              // the padding code (not reported)
+    uint32_t* out;             // [entries]
+};
+hipError_t launch_entry_mask(const EntryMaskArgs& a, hipStream_t st);
 
 // pair_kernel's per-search pair tables, built on the device from the query
 // and the compact-code matrix: main strips (count x (alpha+1)^2 x np dwords)

@@ -544,6 +544,8 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a0) {
     for (int i = 0; i < MW; i++) {
         const uint32_t e = base + (i * 4 + wave) * kMini + lane;   // mini i*4+wave: 64 consecutive entries
         x[i] = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
+        // an upper bound (rare-code merge) is no lower bound of the heap root
+        if (a.emask && e < a.n && (a.emask[e] & a.merge_mask)) x[i] = INT32_MIN;
     }
 #pragma unroll
     for (int i = 0; i < MW; i++) {
@@ -660,6 +662,9 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
         if (x == INT32_MIN || x > t) {
             const uint32_t i = atomicAdd(&a.counters[0], 1u);
             a.cand[i] = make_uint2(e, (uint32_t)x);
+            // a merged-code entry's score is an upper bound: its exact one
+            // comes from the re-score of its lane (FilterArgs::exact_lanes)
+            if (a.emask && (a.emask[e] & a.merge_mask)) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = a.entry_lane[e].y;
         }
     }
     if (!a.host_out) return;
@@ -829,6 +834,29 @@ __global__ void __launch_bounds__(256) pair_addr_kernel(const PairAddrArgs a) {
                                      o[8 * t + 4] | o[8 * t + 5] << 16, o[8 * t + 6] | o[8 * t + 7] << 16);
         cur = nxt;
     }
+}
+
+__global__ void __launch_bounds__(256) entry_mask_kernel(const EntryMaskArgs a) {
+    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (g >= a.ngroups) return;
+    const GroupDesc gd = a.groups[g];
+    const uint32_t nblk = (gd.ncols + 15) >> 4;
+    uint32_t m = 0;
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint4 v = a.res[(size_t)(gd.blk + b) * 64 + lane];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) m |= 1u << ((w[k >> 2] >> (8 * (k & 3))) & 31u);
+    }
+    const uint32_t o = a.lane_out[(size_t)g * 64 + lane];
+    if (o != 0xffffffffu) a.out[o] = m & ~(1u << a.pad);
+}
+
+hipError_t launch_entry_mask(const EntryMaskArgs& a, hipStream_t st) {
+    if (a.ngroups == 0) return hipSuccess;
+    hipLaunchKernelGGL(entry_mask_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_pair_addr(const PairAddrArgs& a, hipStream_t st) {

@@ -1907,3 +1907,57 @@ def test_short_sw_queries_take_32_row_strips():
                 assert S.stats()["strip_rows"] == (48 if m <= 48 else 80), m
             S.free_sequence(qq)
 
+
+
+@pytest.mark.parametrize("algo,gaps,matrix", [(S.SW, (-11, -1), "blosum62"), (S.SW, (-3, -1), "blosum50"),
+                                              (S.NW, (-10, -2), "blosum50")])
+def test_rare_code_merge_exact(algo, gaps, matrix, tmp_path):
+    """Swiss-Prot's rare letters (X, B, Z, U, O) in ~15 % of the entries: the
+    query's residue classes leave a 25-code pair table (two workgroups per
+    CU), so the rarest classes are scored through ONE upper-bound class (the
+    maximum of their rows) and every forwarded entry holding one is
+    re-scored exactly (engine.cpp plan_view, option rare_merge).  Near-copies
+    of the query carry rare letters, so upper bounds reach the top-k and the
+    exact re-score decides it: sw_align / nw_align's top-1/10/64 equal the
+    oracle's (the reference's 64-bit search order), with the merge on and
+    off, and the merge reports what it merged and re-scored."""
+    rng = np.random.default_rng(71 + algo)
+    q = syn.protein_query(300, 13)
+    codes, off = syn.protein_db_range(30000, 91, alphabet="bg20", lengths="uniform", lo=16, hi=700, query=q,
+                                      plant_every=700)
+    codes = codes.copy()
+    rare = np.array([syn.AA_ORDER.index(c) for c in "XBZUO"], np.uint8)
+    lens = np.diff(off).astype(np.int64)
+    n = len(lens)
+    # ~15 % of the entries get 1-3 rare letters; every planted homolog too
+    hit = rng.random(n) < 0.15
+    hit[np.arange(350, n, 700)] = True
+    for i in np.nonzero(hit)[0]:
+        for _ in range(int(rng.integers(1, 4))):
+            codes[int(off[i]) + int(rng.integers(0, lens[i]))] = rare[int(rng.integers(0, 5))]
+    M = TABLES["matrices"][NAMES.index(matrix)].copy()
+    keep = np.nonzero(lens > 0)[0]
+    exp_sc = po.scores(algo, q, codes, off, M, gaps[0], gaps[1])
+    configure(False, ("builtin", matrix), gaps[0], gaps[1])
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    try:
+        for rm in (1, 0):
+            S.set_option("rare_merge", rm)
+            for k in (1, 10, 64):
+                got = [(h["score"], h["id"]) for h in fn(qq, k, 16)]
+                assert got == po.topk(exp_sc[keep], keep.astype(np.uint64), k), (rm, k)
+                st = S.stats()
+                if rm:
+                    assert st["rare_merged"] >= 4 and st["rare_rescored"] > 0, st
+                else:
+                    assert st["rare_merged"] == 0 and st["rare_rescored"] == 0
+        # the log (k = n: no device filter) never merges; its scores are exact
+        S.set_option("rare_merge", 1)
+        sc, ids = _full_scores(qq, algo, n)
+        assert (sc == exp_sc[ids.astype(np.int64)]).all()
+        assert S.stats()["rare_merged"] == 0
+    finally:
+        S.set_option("rare_merge", 1)
+    S.free_sequence(qq)
