@@ -133,9 +133,10 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        for three workgroups per CU, the rarest classes share one class scoring
  *                        the maximum of their rows, and the entries holding them that the device
  *                        filter forwards are re-scored exactly (stats rare_merged / rare_rescored)
- *   "filter_host" 0|1|2  the device filter's result through a D2H copy (0, default) or written by
+ *   "filter_host" 0..3   the device filter's result through a D2H copy (0, default) or written by
  *                        the filter into pinned host memory (1: system-scope release, 2: system-
- *                        scope stores), the host spinning on a sequence word
+ *                        scope stores, the host spinning on a sequence word; 3: plain stores,
+ *                        published by the end of the dispatch, the host synchronising as usual)
  *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
  *                        m_run's INFO line): -1 (default) only at output mode
  *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always

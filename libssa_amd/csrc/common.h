@@ -59,8 +59,10 @@ struct Config {
     int filter_host = 0;                  // 1/2: the top-k filter writes its result into pinned host memory and
                                           // the host spins on its sequence word (no D2H copy, no stream
                                           // synchronisation; 1 with a system-scope release, 2 with system-
-                                          // scope stores and a store-completion wait); 0 (default: 1 measured
-                                          // no gain, profiles/r05/ab/filter_host): copy + hipStreamSynchronize
+                                          // scope stores and a store-completion wait); 3: the filter writes
+                                          // it with plain stores, the host synchronises with the stream (no
+                                          // copy); 0 (default: 1 and 2 measured slower,
+                                          // profiles/r05/ab/filter_host*): copy + hipStreamSynchronize
 };
 Config& cfg();
 // whether a search computes the overflow counters (Config::counters)

@@ -2199,7 +2199,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.host_cap = (uint32_t)std::min<size_t>(D.h_cand_cap, f.n);
                 f.host_seq = D.filter_seq;
                 f.done = gate + 3;
-                f.host_fence = C.filter_host == 1 ? 1u : 0u;
+                f.host_fence = C.filter_host == 1 ? 1u : C.filter_host == 3 ? 2u : 0u;
             }
             const size_t xcap_al = (D.exact_cap + 1) & ~(size_t)1;     // (int64 scores 8-byte aligned)
             if (merge) {
@@ -2266,7 +2266,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         if (parts_used && !perr_in_header)
             check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
         const double t_sync0 = now_ms();
-        if (host_direct) {
+        // filter_host 3: the filter's own stores, made visible by the end of
+        // its dispatch -- an ordinary synchronisation, no copy, no spin
+        const bool spin = host_direct && C.filter_host != 3;
+        if (spin) {
             // spin on the filter's sequence word in pinned memory: the result is
             // here as soon as the last filter block has written it, before the
             // kernel's end-of-dispatch cache writeback and completion signal
@@ -2445,8 +2448,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         }
         check(hipEventElapsedTime(&t, ev_k1, D.ev[2]), "elapsed");
         wms += t;
-        if (!host_direct) {
-            // (the direct path has no copy: the filter's own time is in the
+        if (!spin) {
+            // (the spinning path has no copy: the filter's own time is in the
             // kernel trace, d2h_ms stays 0)
             check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");
             dms += t;

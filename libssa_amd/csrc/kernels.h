@@ -228,7 +228,8 @@ struct FilterArgs {
     uint32_t* done;
     uint32_t host_fence;       // 1: system-scope release before the sequence word (an L2 writeback);
                                // 0: system-scope relaxed stores, each thread waits for its own
-                               // stores' completion before the block's barrier and the sequence word
+                               // stores' completion before the block's barrier and the sequence word;
+                               // 2: plain stores, no ordering (the host synchronises with the stream)
     // rare-code merge (single pass, identity order): an entry whose codes
     // (emask[e]) meet merge_mask holds an UPPER BOUND of its score (the
     // merged class scores the maximum of its members).  It is left out of

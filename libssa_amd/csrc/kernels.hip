@@ -683,6 +683,7 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
         if (a.host_fence) *p = v;
         else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     };
+    // (host_fence 2: the end of the dispatch publishes the plain stores)
     if (threadIdx.x < kFilterSeqWord)
         put(a.host_out + threadIdx.x,
             threadIdx.x == 0 ? nc : __hip_atomic_load(&a.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -696,7 +697,9 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     __syncthreads();
     if (threadIdx.x == 0) {
         *a.done = 0;                           // (the next search's pass counts from 0 again)
-        if (a.host_fence) {
+        if (a.host_fence == 2) {
+            a.host_out[kFilterSeqWord] = a.host_seq;
+        } else if (a.host_fence) {
             __threadfence_system();            // the copies reach host memory before the sequence word
             __hip_atomic_store(a.host_out + kFilterSeqWord, a.host_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {

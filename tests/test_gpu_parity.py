@@ -1040,7 +1040,7 @@ def test_device_filter_candidate_count_is_exact(n, pattern):
             # by the last filter block (with a system-scope release, or with
             # system-scope stores) instead of the D2H copy -- incl. more
             # candidates than the pinned buffer holds ("rising")
-            for fh in (0, 1, 2):
+            for fh in (0, 1, 2, 3):
                 S.set_option("filter_host", fh)
                 for k in (1, 10, 64):
                     got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]

@@ -88,4 +88,15 @@ r5_clock() (
     done
 )
 
+r5_api_trace() (
+    # HIP API + kernel + copy trace of a short C2 run (bench args as $@): the
+    # time between two searches' pair kernels (tools/api_gap.py).  No counters.
+    OUT=$(realpath -m gpurun_out/r5/api${1:+_$1}); mkdir -p "$OUT"; shift
+    REPO=$PWD
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace -d "$OUT" -o run --output-format csv \
+        -- python3 "$REPO/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-north-star "$@" > "$OUT/bench.log" 2>&1
+    python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -3 "$OUT/gap.txt"
+)
+
 "r5_$@"
