@@ -1931,6 +1931,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     b.nparts = parts;
                     b.part_strips = ps;
                     b.nquads = quads;
+                    // option pair_split: only the first P % of the quads (the
+                    // longest, P > 0) or the last -P % (P < 0) are split
+                    b.split_q0 = 0;
+                    b.split_q1 = quads;
+                    if (C.pair_split > 0 && C.pair_split < 100)
+                        b.split_q1 = std::max<uint32_t>(1, (uint32_t)((uint64_t)quads * C.pair_split / 100));
+                    else if (C.pair_split < 0 && C.pair_split > -100)
+                        b.split_q0 = quads - std::max<uint32_t>(1, (uint32_t)((uint64_t)quads * -C.pair_split / 100));
                     b.part_done = D.d_part;
                     b.part_smax = D.d_smax;
                     b.part_err = gate + 2;

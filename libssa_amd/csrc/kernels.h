@@ -91,6 +91,10 @@ struct StripArgs {
     // -- so the SIMDs drain closer together.
     // nparts 1: whole groups, no carry.
     uint32_t nparts, part_strips, nquads;
+    // only quads [split_q0, split_q1) are split (the others run whole as
+    // units 0 .. nquads-1 like part 0): units nquads .. are the later parts
+    // of the split quads, part by part
+    uint32_t split_q0, split_q1;
     uint32_t* part_done;       // [nquads] part_epoch + q once the quad's part q is done (never cleared)
     uint32_t part_epoch;       // this launch's flag base: a multiple of 4, above every earlier launch's values
     uint32_t* part_smax;       // [ngroups * 64]

@@ -146,11 +146,18 @@ pair_kernel(const StripArgs a) {
         wg = u / nqs;
         qi = u - wg * nqs;
     }
-    // strip parts (StripArgs::nparts): unit wg = part `part` of quad wg
+    // strip parts (StripArgs::nparts): units 0 .. nquads-1 are part 0 (or
+    // the whole) of quad wg, later units the later parts of the split quads
     uint32_t part = 0;
+    bool split = false;
     if (a.nparts > 1) {
-        part = wg / a.nquads;
-        wg -= part * a.nquads;
+        const uint32_t ns = a.split_q1 - a.split_q0;
+        if (wg >= a.nquads) {
+            const uint32_t u = wg - a.nquads;
+            part = 1 + u / ns;
+            wg = a.split_q0 + u % ns;
+        }
+        split = wg >= a.split_q0 && wg < a.split_q1;
         if (part > 0) {
             // the group's previous part must be done: its strip boundary rows
             // (row buffer) and running maxima come from that workgroup.  Its
@@ -511,10 +518,10 @@ pair_kernel(const StripArgs a) {
     using TailNP = std::integral_constant<int, NPT ? NPT : 8>;
     // this unit's strips [s0, s1) of the nstrips main strips + the tail strip
     const uint32_t T = a.nstrips + (NPT > 0 ? 1u : 0u);
-    const uint32_t s0 = a.nparts > 1 ? part * a.part_strips : 0u;
-    const uint32_t s1 = a.nparts > 1 ? min(T, s0 + a.part_strips) : T;
+    const uint32_t s0 = split ? part * a.part_strips : 0u;
+    const uint32_t s1 = split ? min(T, s0 + a.part_strips) : T;
     for (uint32_t s = s0; s < min(s1, a.nstrips); s++) {
-        handoff = part + 1 < a.nparts && s + 1 == s1;
+        handoff = split && part + 1 < a.nparts && s + 1 == s1;
         strip(MainNP{}, std::false_type{}, (int)s * 2 * NP, qpt + (size_t)s * prow * prow * NP);
     }
     if (NPT > 0 && s1 == T) {
@@ -522,7 +529,7 @@ pair_kernel(const StripArgs a) {
         strip(TailNP{}, std::integral_constant<bool, NW>{}, (int)a.nstrips * 2 * NP, qpt_tail);
     }
 
-    if (a.nparts > 1 && part + 1 < a.nparts) {
+    if (split && part + 1 < a.nparts) {
         // hand the group on: running maxima, then (after every wave's row
         // buffer stores and maxima are visible at agent scope) the part count
         if (!NW && active) __hip_atomic_store(smax + gl, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -572,9 +579,11 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     if (e != hipSuccess) return e;
     constexpr int W = pair_waves(NP, NW);
     const uint32_t quads = (a.ngroups - a.g_first + W - 1) / W;
-    if (a.nparts > 1 && a.nquads != quads) return hipErrorInvalidValue;
+    if (a.nparts > 1 && (a.nquads != quads || a.split_q0 >= a.split_q1 || a.split_q1 > quads))
+        return hipErrorInvalidValue;
     if (a.nq > (uint32_t)kMaxFuse) return hipErrorInvalidValue;
-    const uint32_t blocks = quads * std::max(a.nparts, 1u) * std::max(a.nq, 1u);
+    const uint32_t units = a.nparts > 1 ? quads + (a.nparts - 1) * (a.split_q1 - a.split_q0) : quads;
+    const uint32_t blocks = units * std::max(a.nq, 1u);
     hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }
