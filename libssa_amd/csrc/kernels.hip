@@ -1656,14 +1656,14 @@ hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
 
 
 // pair_sw.hip / pair_nw.hip
-hipError_t launch_pair_sw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st);
-hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st);
+hipError_t launch_pair_sw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st, int* occ);
+hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st, int* occ);
 
-hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st) {
-    if (a.ngroups <= a.g_first || (a.nstrips == 0 && npt == 0)) return hipSuccess;
+hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_bytes, hipStream_t st, int* occ) {
+    if (!occ && (a.ngroups <= a.g_first || (a.nstrips == 0 && npt == 0))) return hipSuccess;
     // NW scores come from the tail strip's capture
     if (nw && npt == 0) return hipErrorInvalidValue;
-    return nw ? launch_pair_nw(a, np, npt, lds_bytes, st) : launch_pair_sw(a, np, npt, lds_bytes, st);
+    return nw ? launch_pair_nw(a, np, npt, lds_bytes, st, occ) : launch_pair_sw(a, np, npt, lds_bytes, st, occ);
 }
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {

@@ -573,11 +573,13 @@ pair_kernel(const StripArgs a) {
 }
 
 template <int NP, bool NW, int NPT>
-static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st) {
+static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_t st, int* occ) {
     static std::atomic<uint64_t> attr{0};
     const hipError_t e = lds_attr_once((const void*)pair_kernel<NP, NW, NPT>, attr, (int)kPairLdsMax);
     if (e != hipSuccess) return e;
     constexpr int W = pair_waves(NP, NW);
+    if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)pair_kernel<NP, NW, NPT>, 64 * W,
+                                                                 lds_bytes);
     const uint32_t quads = (a.ngroups - a.g_first + W - 1) / W;
     if (a.nparts > 1 && (a.nquads != quads || a.split_q0 >= a.split_q1 || a.split_q1 > quads))
         return hipErrorInvalidValue;
@@ -589,13 +591,13 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
 }
 
 template <int NP, bool NW, int NPT = 4>
-static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st) {
+static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st, int* occ) {
     // npt in {0} + multiples of 4 up to NP
     if constexpr (NPT == 4) {
-        if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st);
+        if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st, occ);
     }
-    if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st);
-    if constexpr (NPT + 4 <= NP) return launch_pair_np<NP, NW, NPT + 4>(a, npt, lds_bytes, st);
+    if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st, occ);
+    if constexpr (NPT + 4 <= NP) return launch_pair_np<NP, NW, NPT + 4>(a, npt, lds_bytes, st, occ);
     return hipErrorInvalidValue;
 }
 

@@ -5,13 +5,13 @@
 
 namespace ssa {
 
-hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st) {
+hipError_t launch_pair_nw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st, int* occ) {
     switch (np) {
-    case 24: return launch_pair_np<24, true>(a, npt, lds_bytes, st);
-    case 32: return launch_pair_np<32, true>(a, npt, lds_bytes, st);
-    case 40: return launch_pair_np<40, true>(a, npt, lds_bytes, st);
-    case 16: return launch_pair_np<16, true>(a, npt, lds_bytes, st);
-    case 8: return launch_pair_np<8, true>(a, npt, lds_bytes, st);
+    case 24: return launch_pair_np<24, true>(a, npt, lds_bytes, st, occ);
+    case 32: return launch_pair_np<32, true>(a, npt, lds_bytes, st, occ);
+    case 40: return launch_pair_np<40, true>(a, npt, lds_bytes, st, occ);
+    case 16: return launch_pair_np<16, true>(a, npt, lds_bytes, st, occ);
+    case 8: return launch_pair_np<8, true>(a, npt, lds_bytes, st, occ);
     default: return hipErrorInvalidValue;
     }
 }

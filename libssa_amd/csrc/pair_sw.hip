@@ -5,14 +5,14 @@
 
 namespace ssa {
 
-hipError_t launch_pair_sw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st) {
+hipError_t launch_pair_sw(const StripArgs& a, int np, int npt, size_t lds_bytes, hipStream_t st, int* occ) {
     switch (np) {
-    case 24: return launch_pair_np<24, false>(a, npt, lds_bytes, st);
-    case 32: return launch_pair_np<32, false>(a, npt, lds_bytes, st);
-    case 36: return launch_pair_np<36, false>(a, npt, lds_bytes, st);
-    case 40: return launch_pair_np<40, false>(a, npt, lds_bytes, st);
-    case 16: return launch_pair_np<16, false>(a, npt, lds_bytes, st);
-    case 8: return launch_pair_np<8, false>(a, npt, lds_bytes, st);
+    case 24: return launch_pair_np<24, false>(a, npt, lds_bytes, st, occ);
+    case 32: return launch_pair_np<32, false>(a, npt, lds_bytes, st, occ);
+    case 36: return launch_pair_np<36, false>(a, npt, lds_bytes, st, occ);
+    case 40: return launch_pair_np<40, false>(a, npt, lds_bytes, st, occ);
+    case 16: return launch_pair_np<16, false>(a, npt, lds_bytes, st, occ);
+    case 8: return launch_pair_np<8, false>(a, npt, lds_bytes, st, occ);
     default: return hipErrorInvalidValue;
     }
 }
