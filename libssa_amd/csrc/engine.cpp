@@ -938,8 +938,9 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     bool use_cls = C.sw_kernel == 0 && np == 16 && cls_rep.size() < D.alpha &&
                    pair_wgs(cls_rep.size()) > pair_wgs(D.alpha);
     // Rare-code merge (Swiss-Prot's X, B, Z, U, O: ~0.04 % of the residues,
-    // in ~12 % of the entries): when the classes still leave the pair table
-    // too big for three workgroups per CU, the rarest classes share ONE class
+    // in ~12 % of the entries): when the classes leave the pair table too big
+    // for the best plan (SW: three workgroups per CU; NW: 80-row strips at
+    // two), the fewest rarest classes that reach it share ONE class
     // that scores the element-wise maximum of their rows.  An entry holding
     // one of them then scores an upper bound of its true score (max-plus DP
     // is monotone in the profile); the device filter leaves such entries out
@@ -958,7 +959,7 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
                 xhi = std::max(xhi, x);
             }
         const int rlx = rescore32_rl(D, m, D.alpha, C.gap_open, C.gap_extend, xlo, xhi);
-        if (rlx > 0 && pair_wgs(A0).first < 3 && A0 >= 3) {
+        if (rlx > 0 && A0 >= 3) {
             std::vector<uint64_t> ce(A0, 0);
             for (uint32_t c = 0; c < D.alpha; c++) ce[cls_of[c]] += D.code_entries[c];
             std::vector<uint32_t> ord(A0);
@@ -968,7 +969,9 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
             for (size_t k = 2; k < A0; k++) {
                 fl += ce[ord[k - 1]];
                 if (fl * 4 > D.meta.size()) break;
-                if (pair_wgs(A0 - k + 1).first < 3) continue;
+                // (workgroups per CU, then strip height: SW 2 -> 3 workgroups
+                // per CU, NW 64 -> 80-row strips at two per CU)
+                if (!(pair_wgs(A0 - k + 1) > pair_wgs(A0))) continue;
                 // classes ord[0..k) become one: the others keep their order,
                 // the merged class comes last
                 std::vector<uint8_t> merged(A0, 0), idx(A0, 0);

@@ -113,24 +113,6 @@ struct StripArgs {
     uint32_t nq;
     const uint32_t* qm;
     size_t q_tab_stride, q_score_stride, q_ovf_stride, q_rowbuf_stride;
-    // pair_kernel, resident-slot row buffers: a work unit
-    // keeps its own strip boundaries in a slot it takes from its XCD's pool
-    // when it starts (a busy bit in slot_bits, XCC_ID-indexed) and returns
-    // when it ends, so the boundary memory is sized to the workgroups in
-    // flight, not to the DB: slots_per_xcd x 4 waves x slot_blocks residue
-    // blocks of 4 KiB.  A slot is reused only on its own XCD (one L2; the
-    // row loads are nt, L1-bypassing).  The boundary a strip part hands to
-    // the next part (maybe on another XCD) goes through `handoff` instead:
-    // part k -> k + 1 at handoff + k * handoff_part_stride + qi *
-    // q_handoff_stride + (group blk - handoff_blk0) * 256, each address
-    // written once per launch (the split quads' groups only).  slots null:
-    // rowbuf / rowbuf2 / rowbuf3 above, indexed by group.
-    uint4* slots;
-    unsigned long long* slot_bits;   // [8 XCDs][slot_words]
-    uint32_t slots_per_xcd, slot_words, slot_blocks;
-    uint32_t handoff_blk0;
-    uint4* handoff;
-    size_t handoff_part_stride, q_handoff_stride;
     // pair_kernel: the pair-row stream (pair_addr_kernel), the LDS offset of
     // each column's next pair row in 16-byte units, 16 bits per column, in
     // octs of 8 columns (2 KiB per residue block), built for this launch's

@@ -289,12 +289,17 @@ pair_kernel(const StripArgs a) {
         // itself: diagonal input Q+4R plus the padding profile -2R, E and F at
         // the pattern minimum, so h = Q+2R and E leaves it as h+Q.
         // SW, also diagonal-relative: true 0 is the pattern of (i+j)|R|, so
-        // the local-alignment floor differs per row and column: fl[r] holds
-        // the floor of the next column for both halves of row r (wave-
-        // uniform, SGPRs, +|R| per column).  Boundary H(i,-1) = 0 ->
+        // the local-alignment floor differs per row and column: row r's
+        // floor of the next column, both halves, is fl0 + r|R| (fl0: row 0's,
+        // wave-uniform, +|R| per column) -- walked down the rows by one
+        // scalar add per row (flr), so one SGPR holds the floors instead of
+        // NPS (the column loop's SGPRs are the tight resource: spilled ones
+        // come back as v_readlane in the loop).  Boundary H(i,-1) = 0 ->
         // (i-1)|R|; high halves at step 0: E at the boundary value, the
         // diagonal input and F low, so h = (i-1)|R|.
-        uint32_t H[NPS], E[NPS], fl[NPS];
+        uint32_t H[NPS], E[NPS];
+        uint32_t fl0 = NW ? 0u : __builtin_amdgcn_readfirstlane(pat((i0 + 1) * (int)Rabs) |
+                                                                (pat((i0 + NPS) * (int)Rabs) << 16));
 #pragma unroll
         for (int r = 0; r < NPS; r++) {
             if (NW) {
@@ -303,8 +308,6 @@ pair_kernel(const StripArgs a) {
             } else {
                 H[r] = pat((i0 + r - 1) * (int)Rabs) | (pat(0) << 16);
                 E[r] = pat((i0 + r) * (int)Rabs) | (pat((i0 + NPS + r - 1) * (int)Rabs) << 16);
-                fl[r] = __builtin_amdgcn_readfirstlane(pat((i0 + r + 1) * (int)Rabs) |
-                                                       (pat((i0 + NPS + r) * (int)Rabs) << 16));
             }
         }
         // diagonal input of row i0 at column 0, H(i0-1, -1); high half low
@@ -326,12 +329,9 @@ pair_kernel(const StripArgs a) {
         // the previous column's H of the row below (one max3 per two cells);
         // the group's anti-diagonal g+j is complete after its first row at
         // column j and is flushed into S with one saturating subtract of its
-        // floor (= that row's floor fl[g]).  G divides the 16-column block, so
+        // floor (= that row's floor).  G divides the 16-column block, so
         // every register index is static.
         constexpr bool AD = !NW;
-        // floors advance right after their row's last use (fewer live SGPRs;
-        // measured neutral at 16 rows, -0.7 % at 24, where they fit anyway)
-        constexpr bool FL_INROW = NPS <= 16;
         constexpr int NG = ad_ngroups(NPS);
         uint32_t A[AD ? NPS : 1];
 #pragma unroll
@@ -362,9 +362,14 @@ pair_kernel(const StripArgs a) {
         uint32_t P[NPS];
         {
             // column 0's pair (d_0, pad) is not in LDS (pair_lds_row): the
-            // global table's row, from L2, once per strip
+            // row (d_0, 0) with its high halves replaced by the padding
+            // value -- a combined constant lo + 65536 hi with a signed low
+            // half, so lo is the sign-extended low 16 bits
             const uint32_t d0 = resp[0].x & 0xffu;
-            load_row<NPS>(P, tab + (size_t)(d0 * prow + a.alpha) * NPS);
+            load_row<NPS>(P, (const uint32_t*)((const char*)lds + pair_lds_row(a.alpha, d0, 0) * (ROWW * 4)));
+            const uint32_t hi = (uint32_t)(int32_t)(int16_t)(a.pad_word & 0xffffu) << 16;
+#pragma unroll
+            for (int r = 0; r < NPS; r++) P[r] = (uint32_t)(int32_t)(int16_t)(P[r] & 0xffffu) + hi;
         }
 
         for (uint32_t b = 0; b < nblk; b++) {
@@ -405,6 +410,7 @@ pair_kernel(const StripArgs a) {
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
                     uint32_t xs[2];
+                    uint32_t flr = fl0;          // row r's floor (SW), advanced row by row
 #pragma unroll
                     for (int r = 0; r < NPS; r++) {
                         // the diagonal step: P holds combined signed constants
@@ -434,18 +440,18 @@ pair_kernel(const StripArgs a) {
                             F = fmax2(F, tt);
                         } else {
                             const uint32_t tt = h + cQ;
-                            E[r] = fmax3(E[r], tt, fl[r]);
+                            E[r] = fmax3(E[r], tt, flr);
                             F = fmax2(F, tt);
                             if (!AD) {
                                 // x = max(H - |R|, 0) into H[r]'s slot of the S tree
-                                xs[r & 1] = psubsat16(h, fl[r]);
+                                xs[r & 1] = psubsat16(h, flr);
                                 if (r & 1) S = fmax3(S, xs[0], xs[1]);
                             }
                             if (AD && r == g0) {
                                 // the group's anti-diagonal g0+j is complete:
                                 // x = max(H - |R|, 0).  One group: S takes two
                                 // columns' x per max3; several: two groups'.
-                                const uint32_t x = psubsat16(A[g0 + k % G], fl[g0]);
+                                const uint32_t x = psubsat16(A[g0 + k % G], flr);   // (r == g0)
                                 const int gi = ad_index(r, NPS);
                                 if (NG == 1) {
                                     xa[k & 1] = x;
@@ -458,15 +464,13 @@ pair_kernel(const StripArgs a) {
                                     xa[0] = x;
                                 }
                             }
-                            // row r's floor for the next column, updated in
-                            // place right after its last use (SGPRs are tight)
-                            if (FL_INROW) fl[r] += cRabs;
+                            // the next row's floor (a chain the compiler
+                            // must not turn into NPS precomputed values)
+                            flr += cRabs;
+                            asm volatile("" : "+s"(flr));
                         }
                     }
-                    if (!NW && !FL_INROW) {
-#pragma unroll
-                        for (int r = 0; r < NPS; r++) fl[r] += cRabs;
-                    }
+                    if (!NW) fl0 += cRabs;
                     hd0 = perm(hd, rbv, SEL_LO_BLO_HI_ALO);
                     Fprev = F;
                     // a per-step anchor the scheduler cannot move work across
@@ -499,16 +503,17 @@ pair_kernel(const StripArgs a) {
         if (AD) {
             // drain after the last column J = ncols-1: the odd local rows'
             // cells of column J, and each group's anti-diagonals J+1 ..
-            // J+G-1 (partial).  fl[] now hold column J+1's floors; register
-            // g+p holds the group's anti-diagonal J+1+d, d = (p - ncols) mod G,
-            // floor fl[g] + d|R| (d = G-1 is anti-diagonal J, already
-            // flushed: skipped).
+            // J+G-1 (partial).  fl0 now holds column J+1's floor of row 0;
+            // register g+p holds the group's anti-diagonal J+1+d, d = (p -
+            // ncols) mod G, floor fl0 + (g + d)|R| (d = G-1 is anti-diagonal
+            // J, already flushed: skipped).
 #pragma unroll
             for (int r = 0; r < NPS; r++) {
                 const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
-                if ((r - g0) & 1) S = fmax2(S, psubsat16(H[r], fl[r] - cRabs));
+                // (fl0 + r|R|: row r's floor of column J+1)
+                if ((r - g0) & 1) S = fmax2(S, psubsat16(H[r], fl0 + (uint32_t)(r - 1) * cRabs));
                 const uint32_t d = ((uint32_t)(r - g0) - gd.ncols) & (G - 1);
-                const uint32_t f = d == (uint32_t)G - 1 ? 0xffffffffu : fl[g0] + d * cRabs;
+                const uint32_t f = d == (uint32_t)G - 1 ? 0xffffffffu : fl0 + ((uint32_t)g0 + d) * cRabs;
                 S = fmax2(S, psubsat16(A[r], __builtin_amdgcn_readfirstlane(f)));
             }
         }

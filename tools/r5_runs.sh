@@ -99,4 +99,23 @@ r5_api_trace() (
     python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -3 "$OUT/gap.txt"
 )
 
+r5_libab() (
+    # alternating A/B of two library builds: A = libssa_amd/lib (this tree),
+    # B = libssa_amd/lib_ab; $1 = name, $2.. = configs, REPS (default 2)
+    name=$1; shift
+    mkdir -p gpurun_out/r5/libab/$name
+    A=$PWD/libssa_amd/lib/libssa_amd.so
+    B=$PWD/libssa_amd/lib_ab/libssa_amd.so
+    for i in $(seq 1 ${REPS:-2}); do
+        for cfg in "$@"; do
+            for v in A B; do
+                if [ $v = A ]; then L=$A; else L=$B; fi
+                SSA_AMD_LIB=$L timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-north-star --no-cpu-baseline \
+                    > gpurun_out/r5/libab/$name/${cfg}_${v}_$i.json 2> gpurun_out/r5/libab/$name/${cfg}_${v}_$i.err || { tail -20 gpurun_out/r5/libab/$name/${cfg}_${v}_$i.err; exit 1; }
+                python -c "import json; d=json.loads(open('gpurun_out/r5/libab/$name/${cfg}_${v}_$i.json').read().strip().splitlines()[-1]); print('$name $cfg $v$i', d['value'], d['kernel']['kernel_gcups'], d['ms_per_step'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+            done
+        done
+    done
+)
+
 "r5_$@"
