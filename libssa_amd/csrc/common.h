@@ -53,6 +53,8 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
+    int side_tier = 1;                    // 1: the int32 re-score tier runs beside the device filter (a second
+                                          // stream) instead of in front of it (single-view sparse searches)
     int pair_split = 0;                   // strip parts for all quads (0) or only the first P % (P > 0, the longest)
                                           // or the last -P % (P < 0) of the quads
     int rare_merge = 1;                   // 1: when the query's residue classes leave the pair table too big for

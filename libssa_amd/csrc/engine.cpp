@@ -1649,6 +1649,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
 
         // the int32 re-score tier for this view's overflowed lanes, when exact
         const int rl32 = rescore32_rl(D, m, A, Q, R, minM, maxM);
+        // the int32 tier beside the filter (on stream_long1, after the DP
+        // kernels) instead of in front of it: the filter does not read its
+        // output, so the tier leaves the path from the pair kernel's end to
+        // the result; the tables kernel then clears the filter header
+        const bool side_tier = C.side_tier && rl32 > 0 && use_pair && out.sparse && !piped && !want_counts;
         LongArgs ra{};
         if (rl32 > 0) {
             ra.res = dres;
@@ -1831,6 +1836,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
             ta.zero = ovf;
+            if (side_tier) {
+                ta.zero_hdr = D.d_fbuf;
+                ta.nzero_hdr = kFilterHeader;
+            }
             // the start-order ticket (StripArgs::ticket): always with strip
             // parts, whose waits rely on it
             {
@@ -2023,7 +2032,12 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
             if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
             check(hipEventRecord(ev_k1, st), "event");
-            if (rl32 > 0) {
+            if (side_tier) {
+                // (header cleared by the tables kernel; no counters)
+                check(hipStreamWaitEvent(D.stream_long1, ev_k1, 0), "event wait");
+                check(launch_long(ra, 1, rl32, nw, D.stream_long1), "int32 re-score launch");
+                check(hipEventRecord(D.ev[8], D.stream_long1), "event");
+            } else if (rl32 > 0) {
                 // the int32 tier clears what wide_kernel would have (one launch)
                 LongArgs rz = ra;
                 rz.zero = w.zero;
@@ -2220,6 +2234,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.exact_lanes = D.d_exact;
             }
             check(launch_filter(f, st), "filter launch");
+            // (the stream's end, and so the host's wake-up, covers the tier)
+            if (side_tier) check(hipStreamWaitEvent(st, D.ev[8], 0), "event wait");
             if (merge) {
                 // the forwarded merged-code entries, exactly: the int32 tier
                 // over their lanes (count: the filter header's word 1) on the
@@ -2457,7 +2473,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
             kms += t;
         }
-        check(hipEventElapsedTime(&t, ev_k1, D.ev[2]), "elapsed");
+        check(hipEventElapsedTime(&t, ev_k1, side_tier ? D.ev[8] : D.ev[2]), "elapsed");
         wms += t;
         if (!spin) {
             // (the spinning path has no copy: the filter's own time is in the

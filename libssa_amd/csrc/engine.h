@@ -28,7 +28,7 @@ struct DeviceDB {
     uint64_t generation = ~0ull;
     int symtype = -1, strands = -1, dgencode = -1;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[9] = {};                // [8]: the int32 tier's end when it runs beside the filter
     EntryMeta meta;
     uint32_t ngroups = 0;
     uint64_t nblocks = 0;                 // 1 KiB residue blocks

@@ -393,6 +393,8 @@ struct TableArgs {
     const uint32_t* gate;
     uint32_t gate_target;
     uint32_t* zero_ticket;     // StripArgs::ticket, cleared by thread 0 (may be null)
+    uint32_t* zero_hdr;        // nzero_hdr dwords cleared by block 0 (the filter pass's counters,
+    uint32_t nzero_hdr;        // when the re-score tier runs beside the filter instead of before it)
 };
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
 

@@ -730,6 +730,7 @@ __device__ __forceinline__ int32_t table_val(const TableArgs& a, uint32_t c, uin
 __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
     if (a.zero && blockIdx.x == 0 && threadIdx.x == 0) *a.zero = 0;
     if (a.zero_ticket && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_ticket = 0;
+    if (a.zero_hdr && blockIdx.x == 0 && threadIdx.x < a.nzero_hdr) a.zero_hdr[threadIdx.x] = 0;
     if (a.gate && blockIdx.x == 0 && threadIdx.x == 0) {
         // the long entries' workgroups (another stream) start first; bounded
         // at ~20 ms of the 100 MHz real-time counter, so a gate that is never
@@ -768,6 +769,10 @@ hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const uint32_t prow = a.alpha + 1;
     const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);
     if (total == 0) {
+        if (a.zero_hdr) {
+            const hipError_t e = hipMemsetAsync(a.zero_hdr, 0, 4 * a.nzero_hdr, st);
+            if (e != hipSuccess) return e;
+        }
         if (a.zero_ticket) {
             const hipError_t e = hipMemsetAsync(a.zero_ticket, 0, 4, st);
             if (e != hipSuccess) return e;
