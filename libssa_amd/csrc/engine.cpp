@@ -886,6 +886,9 @@ struct ViewPlan {
     uint32_t merge_mask = 0;
     uint64_t merge_entries = 0;
     int merge_rl = 0;
+    // the compact codes' profile bounds (the exact re-score's and, with a
+    // merge, the long-entry kernels', which score the compact codes exactly)
+    int64_t xminM = 0, xmaxM = 0;
 };
 struct PlanForce {
     int64_t minM, maxM;
@@ -993,6 +996,8 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
                 cls_rep = std::move(rep2);
                 vp.merge_entries = fl;
                 vp.merge_rl = rlx;
+                vp.xminM = xlo;
+                vp.xmaxM = xhi;
                 use_cls = true;
                 break;
             }
@@ -1053,7 +1058,11 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
         if (lim > 0) {
             const size_t beyond = (size_t)(D.len_sorted.end() -
                                            std::upper_bound(D.len_sorted.begin(), D.len_sorted.end(), lim));
-            const uint32_t lg = long_plan(D, ml, beyond, Q, R, minM, maxM, force ? force->long_scale : 1u);
+            // (with a merge the long-entry kernels score the compact codes:
+            // their bound covers both profiles)
+            const int64_t lminM = vp.merge_mask ? std::min(minM, vp.xminM) : minM;
+            const int64_t lmaxM = vp.merge_mask ? std::max(maxM, vp.xmaxM) : maxM;
+            const uint32_t lg = long_plan(D, ml, beyond, Q, R, lminM, lmaxM, force ? force->long_scale : 1u);
             // (an entry beyond the bound would also corrupt its group's
             // other lanes, whose padding columns run to its length: the
             // group must go to long_kernel, or the strip kernels run)
@@ -1708,7 +1717,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
         size_t lds_long = pair_lds;   // LDS of a long workgroup (the pair tables' gate)
         if (long_groups > 0) {
-            const int rl16 = long16_plan(D, m, nw, Q, R, minM, maxM);
+            // a merge: the long entries are scored exactly on the compact codes
+            // (a 35 k-residue entry re-scored by one wave would cost
+            // milliseconds), so they never need the exact re-score
+            const int rl16 = merge ? long16_plan(D, m, nw, Q, R, std::min(minM, vp.xminM), std::max(maxM, vp.xmaxM))
+                                   : long16_plan(D, m, nw, Q, R, minM, maxM);
             // the longest groups on their own streams, concurrently with the
             // pair kernel (enqueued first, so their waves start first): one
             // wave per entry (RL rows per lane, 64*RL rows per pass), or --
@@ -1724,15 +1737,15 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 while (long4 < long_groups && D.group_ncols[long4] > thr4) long4++;
             }
             LongArgs la{};
-            la.res = dres;
+            la.res = merge ? D.d_res : dres;
             la.groups = D.d_groups;
             la.lane_len = D.d_lane_len;
             la.lane_out = D.d_lane_out;
             la.query = D.d_query;
-            la.matrix = D.d_matrix;
+            la.matrix = merge ? (const int64_t*)(dup + kUpExactMat) : D.d_matrix;
             la.scores = a.scores;
             la.m = (uint32_t)m;
-            la.alpha = A;
+            la.alpha = merge ? D.alpha : A;
             la.gap_open = Q;
             la.gap_extend = R;
             // NW: the exact extremes of H the overflow counters decide from,
@@ -2232,6 +2245,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.merge_mask = vp.merge_mask;
                 f.entry_lane = (const uint2*)D.d_entry_lane;
                 f.exact_lanes = D.d_exact;
+                f.exact_lane0 = long_groups * 64;
             }
             check(launch_filter(f, st), "filter launch");
             // (the stream's end, and so the host's wake-up, covers the tier)

@@ -244,6 +244,7 @@ struct FilterArgs {
     uint32_t merge_mask;
     const uint2* entry_lane;
     uint32_t* exact_lanes;
+    uint32_t exact_lane0;      // lanes below it (the long-entry kernels') are scored exactly anyway
 };
 constexpr int kFilterSeqWord = 15;    // header word that carries FilterArgs::host_seq
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

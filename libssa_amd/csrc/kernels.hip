@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(256) filter_block(const FilterArgs a0) {
         const uint32_t e = base + (i * 4 + wave) * kMini + lane;   // mini i*4+wave: 64 consecutive entries
         x[i] = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
         // an upper bound (rare-code merge) is no lower bound of the heap root
-        if (a.emask && e < a.n && (a.emask[e] & a.merge_mask)) x[i] = INT32_MIN;
+        if (a.emask && e < a.n && (a.emask[e] & a.merge_mask) && a.entry_lane[e].y >= a.exact_lane0) x[i] = INT32_MIN;
     }
 #pragma unroll
     for (int i = 0; i < MW; i++) {
@@ -664,7 +664,10 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
             a.cand[i] = make_uint2(e, (uint32_t)x);
             // a merged-code entry's score is an upper bound: its exact one
             // comes from the re-score of its lane (FilterArgs::exact_lanes)
-            if (a.emask && (a.emask[e] & a.merge_mask)) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = a.entry_lane[e].y;
+            if (a.emask && (a.emask[e] & a.merge_mask)) {
+                const uint32_t l = a.entry_lane[e].y;
+                if (l >= a.exact_lane0) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = l;
+            }
         }
     }
     if (!a.host_out) return;
