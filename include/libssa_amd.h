@@ -129,7 +129,7 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "part_wait_us" N     bound of a strip part's wait for its group's first part (default
  *                        2000000); a timed-out wait makes the search run again without parts
  *                        (stats part_retries), results unchanged
- *   "rare_merge" 1|0     1 (default): when a query's residue classes leave the pair table too big
+ *   "rare_merge" 0|1     1 (default 0): when a query's residue classes leave the pair table too big
  *                        for three workgroups per CU, the rarest classes share one class scoring
  *                        the maximum of their rows, and the entries holding them that the device
  *                        filter forwards are re-scored exactly (stats rare_merged / rare_rescored)
@@ -137,6 +137,12 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        the filter into pinned host memory (1: system-scope release, 2: system-
  *                        scope stores, the host spinning on a sequence word; 3: plain stores,
  *                        published by the end of the dispatch, the host synchronising as usual)
+ *   "sync_spin" 1|0      1 (default): the host spins while a search runs (hipDeviceScheduleSpin, set
+ *                        at the library's first pack on a device); 0: HIP's default (yield)
+ *   "side_tier" 0|1      1: the int32 re-score tier runs beside the device filter on a second
+ *                        stream instead of in front of it (default 0: no gain measured)
+ *   "pair_split" P       strip parts for every quad of groups (0, default) or only the first P %
+ *                        (the longest, P > 0) or the last -P % (P < 0)
  *   "counters" -1|0|1    the reference's 8/16-bit overflow counters (stats overflow_8/16,
  *                        m_run's INFO line): -1 (default) only at output mode
  *                        OUTPUT_INFO, where the reference prints them; 0 never; 1 always

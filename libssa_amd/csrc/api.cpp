@@ -447,6 +447,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "rare_merge")) cfg().rare_merge = (int)value;
     else if (!strcmp(name, "pair_split")) cfg().pair_split = (int)value;
     else if (!strcmp(name, "side_tier")) cfg().side_tier = (int)value;
+    else if (!strcmp(name, "sync_spin")) cfg().sync_spin = (int)value;
     else print_warning("unknown option %s", name);
 }
 

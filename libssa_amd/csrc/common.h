@@ -53,13 +53,18 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
-    int side_tier = 1;                    // 1: the int32 re-score tier runs beside the device filter (a second
-                                          // stream) instead of in front of it (single-view sparse searches)
+    int sync_spin = 1;                    // 1: hipDeviceScheduleSpin for this library's devices (set at the first
+                                          // pack on a device): the host spins, not yields, while a search runs
+    int side_tier = 0;                    // 1: the int32 re-score tier runs beside the device filter (a second
+                                          // stream) instead of in front of it (single-view sparse searches;
+                                          // measured no gain, profiles/r05/ab/side_tier)
     int pair_split = 0;                   // strip parts for all quads (0) or only the first P % (P > 0, the longest)
                                           // or the last -P % (P < 0) of the quads
-    int rare_merge = 1;                   // 1: when the query's residue classes leave the pair table too big for
+    int rare_merge = 0;                   // 1: when the query's residue classes leave the pair table too big for
                                           // three workgroups per CU, the rarest classes share one upper-bound
                                           // class and the forwarded entries holding them are re-scored exactly
+                                          // (default off: Swiss-Prot form kernel +0.8 %, end to end -4 %,
+                                          // profiles/r05/ab/merge_sprot2)
     int filter_host = 0;                  // 1/2: the top-k filter writes its result into pinned host memory and
                                           // the host spins on its sequence word (no D2H copy, no stream
                                           // synchronisation; 1 with a system-scope release, 2 with system-

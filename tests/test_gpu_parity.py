@@ -1532,15 +1532,19 @@ def test_fullsize_matches_reference_hash(name, tmp_path):
         assert got == c[f"top{k}"], k
         st = S.stats()
         assert [st["overflow_8"], st["overflow_16"]] == c["overflow"], k
-    # without the counters (the benchmark's OUTPUT_ERROR): the searches that
-    # may take the rare-code merge (Swiss-Prot's 25 symbols) -- same top-k
+    # without the counters (the benchmark's OUTPUT_ERROR), with the rare-code
+    # merge allowed (it runs on Swiss-Prot's 25 symbols) -- same top-k
     S.set_option("counters", 0)
-    for k in (1, 10, 64):
-        got = [[h["score"], h["id"]] for h in fn(qq, k, c["width"])]
-        assert got == c[f"top{k}"], ("no counters", k)
-        if c.get("alphabet") == "sprot25" and c["algo"] == "sw":
-            assert S.stats()["rare_merged"] > 0
-    S.set_option("counters", 1)
+    S.set_option("rare_merge", 1)
+    try:
+        for k in (1, 10, 64):
+            got = [[h["score"], h["id"]] for h in fn(qq, k, c["width"])]
+            assert got == c[f"top{k}"], ("no counters", k)
+            if c.get("alphabet") == "sprot25" and c["algo"] == "sw":
+                assert S.stats()["rare_merged"] > 0
+    finally:
+        S.set_option("counters", 1)
+        S.set_option("rare_merge", 0)
     S.free_sequence(qq)
 
 
@@ -1576,11 +1580,13 @@ def test_tie_band_matches_reference_search64(name, tmp_path):
     top = c["top64"]
     assert top[-1][0] == top[-2][0], "the fixture's 64th score is inside a tie band"
     for width in (16, 8):
-        for counters in (1, 0):      # (0: the rare-code merge may run, sp25)
+        for counters in (1, 0):      # (0, with option rare_merge: the merge may run, sp25)
             S.set_option("counters", counters)
+            S.set_option("rare_merge", 1 - counters)
             got = [[h["score"], h["id"]] for h in fn(qq, 64, width)]
             assert got == top, (width, counters, [x for x in zip(got, top) if x[0] != x[1]][:5])
     S.set_option("counters", 1)
+    S.set_option("rare_merge", 0)
     S.free_sequence(qq)
 
 
@@ -1980,6 +1986,6 @@ def test_rare_code_merge_exact(algo, gaps, matrix, tmp_path):
         assert got == po.topk(exp_sc[keep], keep.astype(np.uint64), 10)
         assert S.stats()["rare_merged"] == 0
     finally:
-        S.set_option("rare_merge", 1)
+        S.set_option("rare_merge", 0)
         S.set_option("counters", 1)
     S.free_sequence(qq)
