@@ -139,6 +139,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        published by the end of the dispatch, the host synchronising as usual)
  *   "sync_spin" 1|0      1 (default): the host spins while a search runs (hipDeviceScheduleSpin, set
  *                        at the library's first pack on a device); 0: HIP's default (yield)
+ *   "lean_events" 0|1    1: no timing markers around the upload, the re-score tier and the
+ *                        filter (stats upload_ms, wide_ms, d2h_ms stay 0; kernel_ms kept)
  *   "side_tier" 0|1      1: the int32 re-score tier runs beside the device filter on a second
  *                        stream instead of in front of it (default 0: no gain measured)
  *   "pair_split" P       strip parts for every quad of groups (0, default) or only the first P %

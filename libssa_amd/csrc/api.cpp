@@ -448,6 +448,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "pair_split")) cfg().pair_split = (int)value;
     else if (!strcmp(name, "side_tier")) cfg().side_tier = (int)value;
     else if (!strcmp(name, "sync_spin")) cfg().sync_spin = (int)value;
+    else if (!strcmp(name, "lean_events")) cfg().lean_events = (int)value;
     else print_warning("unknown option %s", name);
 }
 

@@ -55,6 +55,8 @@ struct Config {
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
     int sync_spin = 1;                    // 1: hipDeviceScheduleSpin for this library's devices (set at the first
                                           // pack on a device): the host spins, not yields, while a search runs
+    int lean_events = 0;                  // 1: no timing markers around the upload, the tier and the filter
+                                          // (stats upload_ms / wide_ms / d2h_ms stay 0; kernel_ms kept)
     int side_tier = 0;                    // 1: the int32 re-score tier runs beside the device filter (a second
                                           // stream) instead of in front of it (single-view sparse searches;
                                           // measured no gain, profiles/r05/ab/side_tier)

@@ -1234,6 +1234,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     if (ind && !(out.sparse && V > 1 && V <= kMaxBatchPipe)) fatal("device_search: batch not pipelinable");
     const bool multi = out.sparse && V > 1 && !ind;
     const bool piped = multi || ind;
+    const bool lean = C.lean_events != 0;   // (option "lean_events": no upload/tier/filter markers)
     // the sparse single-pass filter hands its result straight to the host
     // (FilterArgs::host_out) unless something else still has to be copied
     // back on the stream (the overflow counters)
@@ -1609,7 +1610,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 memcpy(up_m + qm_off + 4 * i, &mi, 4);
             }
         if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
-        check(hipEventRecord(D.ev[4], st), "event");
+        if (!lean) check(hipEventRecord(D.ev[4], st), "event");
         if (!qpt.empty())
             check(hipMemcpyAsync(dqpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
         check(hipMemcpyAsync(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
@@ -2216,7 +2217,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                       "D2H candidates");
         }
         if (piped && v + 1 < V) continue;
-        check(hipEventRecord(D.ev[2], st), "event");
+        if (!lean) check(hipEventRecord(D.ev[2], st), "event");
         if (ind) {
             // (filters already enqueued per query)
         } else if (out.sparse) {
@@ -2338,7 +2339,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 __builtin_ia32_pause();
             }
         } else {
-            check(hipEventRecord(D.ev[3], st), "event");
+            if (!lean) check(hipEventRecord(D.ev[3], st), "event");
             check(hipStreamSynchronize(st), "search");
         }
         sync_wait += now_ms() - t_sync0;
@@ -2359,7 +2360,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         }
         const double t_post0 = now_ms();
 
-        {
+        if (!lean) {
             float u;
             check(hipEventElapsedTime(&u, D.ev[4], ev_k0), "elapsed");
             upload += u;
@@ -2495,9 +2496,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
             kms += t;
         }
-        check(hipEventElapsedTime(&t, ev_k1, side_tier ? D.ev[8] : D.ev[2]), "elapsed");
-        wms += t;
-        if (!spin) {
+        if (!lean || side_tier) {
+            check(hipEventElapsedTime(&t, ev_k1, side_tier ? D.ev[8] : D.ev[2]), "elapsed");
+            wms += t;
+        }
+        if (!spin && !lean) {
             // (the spinning path has no copy: the filter's own time is in the
             // kernel trace, d2h_ms stays 0)
             check(hipEventElapsedTime(&t, D.ev[2], D.ev[3]), "elapsed");

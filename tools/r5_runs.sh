@@ -118,4 +118,19 @@ r5_libab() (
     done
 )
 
+r5_sprot_decomp() (
+    # the Swiss-Prot form's factors, one at a time, on one box (2 rounds,
+    # alternating), each with a wave timeline of one extra step
+    mkdir -p gpurun_out/r5/sprot
+    for i in 1 2; do
+        for v in "sprot:--config sprot" "sprot_bg20:--config sprot --alphabet bg20" "sprot_notail:--config sprot --long-tail 0" "ref:--config ref" "c2_548k:--config c2 --seqs 548208" "c2:--config c2"; do
+            name=${v%%:*}; args=${v#*:}
+            timeout -k 10 300 python bench.py $args --steps 20 --warmup 3 --no-north-star --no-cpu-baseline \
+                --timeline gpurun_out/r5/sprot/${name}_$i.npy > gpurun_out/r5/sprot/${name}_$i.json 2> gpurun_out/r5/sprot/${name}_$i.err \
+                || { tail -20 gpurun_out/r5/sprot/${name}_$i.err; exit 1; }
+            python -c "import json; d=json.loads(open('gpurun_out/r5/sprot/${name}_$i.json').read().strip().splitlines()[-1]); print('$name $i', d['value'], d['kernel']['kernel_gcups'], d['ms_per_step'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
+        done
+    done
+)
+
 "r5_$@"
