@@ -523,6 +523,14 @@ def load_shard(S, w, job):
                               setup_s=time.time() - t0)
 
 
+_OPTIONS = {}
+
+
+def lean_events_on():
+    """The library's lean_events option as this run set it (default 1)."""
+    return _OPTIONS.get("lean_events", 1) != 0
+
+
 def timed_steps(S, job, sh, w, steps, warmup, k):
     """W untimed warm-up steps, then exactly K steps between barrier +
     synchronize on both sides; the max over ranks of the elapsed time."""
@@ -570,9 +578,18 @@ def timed_steps(S, job, sh, w, steps, warmup, k):
     else:
         # (a library build without the running totals: SSA_AMD_LIB A/B runs)
         avg = {"kernel_ms": st["kernel_ms"], "search_ms": st["search_ms"]}
-    # (host-side breakdown: the last search's)
+    # (host-side breakdown: the last search's.  The timing markers around the
+    # upload, the re-score tier and the filter are off by default (option
+    # lean_events: they cost ~40 us a search), so one extra untimed local
+    # search with them on fills in the breakdown)
+    lean = lean_events_on()
+    if lean:
+        S.set_option("lean_events", 0)
+        S.align_scores(sh.qq, k, w.width, algo)
+        S.set_option("lean_events", 1)
+    sb = S.stats() if lean else st
     for f in ("wide_ms", "prep_ms", "upload_ms", "sync_wait_ms", "d2h_ms", "replay_ms"):
-        avg[f] = st[f]
+        avg[f] = sb[f]
     ranks = rank_split(job, sh, avg, split, elapsed / steps) if job.world > 1 else None
     return argparse.Namespace(res=res, step=step, elapsed=elapsed, st=st, avg=avg, ranks=ranks)
 
@@ -731,6 +748,7 @@ def main():
     for o in args.option:
         k, v = o.split("=")
         S.set_option(k, int(v))
+        _OPTIONS[k] = int(v)
     if world > 1 and backend == "nccl" and not args.torch_gather:
         setup_native_gather(S, job)
 

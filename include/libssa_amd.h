@@ -39,8 +39,8 @@ typedef struct {
 typedef struct {
     double search_ms;    /* host wall time of the last search call */
     double kernel_ms;    /* HIP-event time of the int16 strip kernels */
-    double wide_ms;      /* HIP-event time of the exact int64 re-score kernel */
-    double d2h_ms;       /* device->host score copy (HIP events) */
+    double wide_ms;      /* HIP-event time of the exact re-score tier (0 under option "lean_events") */
+    double d2h_ms;       /* device filter + result copy (HIP events; 0 under "lean_events") */
     double replay_ms;    /* host top-k replay */
     double pack_ms;      /* DB packing + upload (only when the DB changed) */
     uint64_t cells;      /* sum over queries of qlen * sum of entry lengths */
@@ -53,7 +53,8 @@ typedef struct {
     uint64_t kernel_bytes;   /* algorithmic HBM bytes of the strip kernels */
     char kernel[32];         /* main scoring kernel of the last search, e.g. "pair_f16_sw" */
     double prep_ms;          /* host work before the first kernel launch (profiles, uploads) */
-    double upload_ms;        /* device time of the per-search uploads before the first kernel */
+    double upload_ms;        /* device time of the per-search uploads before the first kernel (0 under
+                                option "lean_events") */
     double sync_wait_ms;     /* host time blocked in the final stream synchronisation */
     uint32_t strip_rows;     /* pair kernel: rows of its main strips (2 x "pair_np"); 0: other kernels */
     uint32_t counters;       /* 1: overflow_8/16 were computed (bit width 64, output mode >= OUTPUT_INFO
@@ -137,10 +138,12 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        the filter into pinned host memory (1: system-scope release, 2: system-
  *                        scope stores, the host spinning on a sequence word; 3: plain stores,
  *                        published by the end of the dispatch, the host synchronising as usual)
- *   "sync_spin" 1|0      1 (default): the host spins while a search runs (hipDeviceScheduleSpin, set
- *                        at the library's first pack on a device); 0: HIP's default (yield)
- *   "lean_events" 0|1    1: no timing markers around the upload, the re-score tier and the
- *                        filter (stats upload_ms, wide_ms, d2h_ms stay 0; kernel_ms kept)
+ *   "sync_spin" 0|1      1: the host spins while a search runs (hipDeviceScheduleSpin, set at the
+ *                        library's first pack on a device); 0 (default): HIP's own scheduling
+ *                        (no difference measured, profiles/r05/ab/sync_spin)
+ *   "lean_events" 1|0    1 (default): no timing markers around the upload, the re-score tier
+ *                        and the filter (stats upload_ms, wide_ms, d2h_ms read 0; kernel_ms
+ *                        kept; C2 +0.5 %, profiles/r05/ab/lean_events); 0: all markers
  *   "side_tier" 0|1      1: the int32 re-score tier runs beside the device filter on a second
  *                        stream instead of in front of it (default 0: no gain measured)
  *   "pair_split" P       strip parts for every quad of groups (0, default) or only the first P %

@@ -387,13 +387,12 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     D.device = dev;
     if (!D.stream) {
         // how the host waits for a search (option "sync_spin"): HIP's default
-        // on a machine with more CPUs than contexts yields the waiting thread
-        // (~20-30 us from the last copy to the host running again,
-        // profiles/r05/api_c2); spinning keeps that thread on its core.  Set
-        // before this library's first use of the device; a context another
-        // runtime user made first keeps its flags (the call's error is cleared)
-        if (hipSetDeviceFlags(C.sync_spin ? hipDeviceScheduleSpin : hipDeviceScheduleAuto) != hipSuccess)
-            (void)hipGetLastError();
+        // on a machine with more CPUs than contexts yields the waiting thread;
+        // spinning keeps it on its core (no end-to-end difference measured,
+        // profiles/r05/ab/sync_spin, so off by default).  Set before this
+        // library's first use of the device; a context another runtime user
+        // made first keeps its flags (the call's error is cleared)
+        if (C.sync_spin && hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
         check(hipStreamCreateWithFlags(&D.stream_long, hipStreamNonBlocking), "hipStreamCreate");
         check(hipStreamCreateWithFlags(&D.stream_long1, hipStreamNonBlocking), "hipStreamCreate");

@@ -696,6 +696,7 @@ def test_int32_rescore_tier_vs_oracle(algo, qlen, n):
     exp = po.scores(algo, q, codes, off, M, -1, -1)
     configure(False, ("const", 127, -1), -1, -1)
     S.set_option("counters", 0)          # (timed below: no overflow-counter replays in wide_ms)
+    S.set_option("lean_events", 0)       # (wide_ms needs the tier's markers)
     ms = {}
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, codes, off))
@@ -719,6 +720,7 @@ def test_int32_rescore_tier_vs_oracle(algo, qlen, n):
             S.set_option("sw_kernel", 0)
             S.set_option("long_groups", -1)
             S.set_option("rescore32", 1)
+            S.set_option("lean_events", 1)
         S.free_sequence(qq)
     # the speed ratio is reported, not asserted (tools/rescore_bench.py
     # measures it; a shared box must not fail an exact test on timing)

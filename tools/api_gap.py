@@ -29,6 +29,10 @@ def main():
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", r.get("Direction", "copy")))
     ev.sort()
     pairs = [e for e in ev if e[2] == "K" and "pair_kernel" in e[3]]
+    gaps = sorted((pairs[i][0] - pairs[i - 1][1]) / 1e3 for i in range(1, len(pairs)))
+    if gaps:
+        print(f"all {len(gaps)} gaps between pair launches (us): median {gaps[len(gaps) // 2]:.1f}, "
+              f"min {gaps[0]:.1f}, max {gaps[-1]:.1f}")
     a, b = pairs[gi - 1], pairs[gi]
     t0 = a[1]
     print(f"gap between pair launches ending {a[1]} and starting {b[0]}: {(b[0] - a[1]) / 1e3:.1f} us")

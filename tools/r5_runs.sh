@@ -122,7 +122,7 @@ r5_sprot_decomp() (
     # the Swiss-Prot form's factors, one at a time, on one box (2 rounds,
     # alternating), each with a wave timeline of one extra step
     mkdir -p gpurun_out/r5/sprot
-    for i in 1 2; do
+    for i in $(seq 1 ${REPS:-2}); do
         for v in "sprot:--config sprot" "sprot_bg20:--config sprot --alphabet bg20" "sprot_notail:--config sprot --long-tail 0" "ref:--config ref" "c2_548k:--config c2 --seqs 548208" "c2:--config c2"; do
             name=${v%%:*}; args=${v#*:}
             timeout -k 10 300 python bench.py $args --steps 20 --warmup 3 --no-north-star --no-cpu-baseline \
@@ -131,6 +131,18 @@ r5_sprot_decomp() (
             python -c "import json; d=json.loads(open('gpurun_out/r5/sprot/${name}_$i.json').read().strip().splitlines()[-1]); print('$name $i', d['value'], d['kernel']['kernel_gcups'], d['ms_per_step'], d['kernel']['avg_ms'], d.get('topk_vs_reference'))"
         done
     done
+)
+
+r5_kgap() (
+    # kernel + copy trace only (no API trace: its own cost inflates the gap)
+    # of 30 C2 searches: the median time from one pair kernel's end to the
+    # next one's start.  $1 = name, bench args after it
+    OUT=$(realpath -m gpurun_out/r5/kgap_$1); mkdir -p "$OUT"; shift
+    REPO=$PWD
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT" -o run --output-format csv \
+        -- python3 "$REPO/bench.py" --steps 30 --warmup 2 --no-cpu-baseline --no-north-star "$@" > "$OUT/bench.log" 2>&1
+    python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -1 "$OUT/gap.txt"
 )
 
 "r5_$@"
