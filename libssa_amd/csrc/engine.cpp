@@ -1817,13 +1817,15 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             if (long4 < long_groups) {
                 la.seq0 = long4 * 64;
                 la.nseq = (long_groups - long4) * 64;
-                gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
-                D.gate_count += (la.nseq + kLongWaves - 1) / kLongWaves;
+                // one entry per wave: four (or long16_waves) entries per workgroup
+                const uint32_t wpg = rl16 > 0 && C.long16_waves == 8 ? 8u : (uint32_t)kLongWaves;
+                gate_total += (la.nseq + wpg - 1) / wpg;
+                D.gate_count += (la.nseq + wpg - 1) / wpg;
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
-                    check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
+                    check(launch_long16(la, rl16, (int)wpg, D.stream_long1), "long kernel launch");
                 } else {
                     check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
                 }

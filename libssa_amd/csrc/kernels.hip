@@ -1376,8 +1376,8 @@ struct PairSlice {
     uint32_t v[(NR + 1) & ~1];
 };
 
-template <int RL>
-__global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs a) {
+template <int RL, int WV>
+__global__ void __launch_bounds__(64 * WV) long16_kernel(const LongArgs a) {
     static_assert(RL % 2 == 0, "rows per lane come in register pairs");
     asm volatile("" ::: "v167");                     // as long_kernel: a pair wave fits where it ran
     extern __shared__ __attribute__((aligned(16))) uint32_t ptab[];   // [code][lane slot][SLW] dwords
@@ -1392,7 +1392,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
         __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t s = blockIdx.x * kLongWaves + wave;   // one entry per wave
+    const uint32_t s = blockIdx.x * WV + wave;           // one entry per wave
     const bool active = s < a.nseq;
     const uint32_t ss = a.seq0 + (active ? s : 0);
     const GroupDesc gd = a.groups[ss >> 6];
@@ -1414,7 +1414,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
         // before this pass's loads
         __threadfence();
         __syncthreads();
-        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * kLongWaves) {
+        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * WV) {
             const uint32_t c = x / CS, rem = x % CS, sl = rem / SLW, k = rem % SLW;
             uint32_t v = padw;
             if (k < (uint32_t)NR && c < a.alpha) {
@@ -1610,32 +1610,39 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
 
 size_t long16_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * long16_slot(rl) * 4; }
 
-template <int RL>
+template <int RL, int WV>
 static hipError_t launch_long16_k(const LongArgs& a, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
     constexpr size_t kDynMax = kPairLdsMax - 8192;
     const size_t need = long16_lds_bytes(a.alpha, RL);
     if (need > kDynMax) return hipErrorInvalidValue;
     const size_t bytes = std::max<size_t>(need, std::min<size_t>(a.lds_min, kDynMax));
-    const hipError_t e = lds_attr_once((const void*)long16_kernel<RL>, attr, (int)kDynMax);
+    const hipError_t e = lds_attr_once((const void*)long16_kernel<RL, WV>, attr, (int)kDynMax);
     if (e != hipSuccess) return e;
-    const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
-    hipLaunchKernelGGL((long16_kernel<RL>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
+    const uint32_t blocks = (a.nseq + WV - 1) / WV;
+    hipLaunchKernelGGL((long16_kernel<RL, WV>), dim3(blocks), dim3(64 * WV), bytes, st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_long16(const LongArgs& a, int rl, hipStream_t st) {
-    if (a.nseq == 0) return hipSuccess;
-    if (a.alpha > 32 || a.base16 < 0x0400u || a.base16 > 0x7BFFu) return hipErrorInvalidValue;
+template <int WV>
+static hipError_t launch_long16_w(const LongArgs& a, int rl, hipStream_t st) {
     switch (rl) {
-        case 4: return launch_long16_k<4>(a, st);
-        case 6: return launch_long16_k<6>(a, st);
-        case 8: return launch_long16_k<8>(a, st);
-        case 10: return launch_long16_k<10>(a, st);
-        case 12: return launch_long16_k<12>(a, st);
-        case 16: return launch_long16_k<16>(a, st);
+        case 4: return launch_long16_k<4, WV>(a, st);
+        case 6: return launch_long16_k<6, WV>(a, st);
+        case 8: return launch_long16_k<8, WV>(a, st);
+        case 10: return launch_long16_k<10, WV>(a, st);
+        case 12: return launch_long16_k<12, WV>(a, st);
+        case 16: return launch_long16_k<16, WV>(a, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_long16(const LongArgs& a, int rl, int waves, hipStream_t st) {
+    if (a.nseq == 0) return hipSuccess;
+    if (a.alpha > 32 || a.base16 < 0x0400u || a.base16 > 0x7BFFu) return hipErrorInvalidValue;
+    if (waves == 8) return launch_long16_w<8>(a, rl, st);
+    if (waves == 4) return launch_long16_w<4>(a, rl, st);
+    return hipErrorInvalidValue;
 }
 
 // ------------------------------------------------------------------ launch

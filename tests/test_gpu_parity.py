@@ -474,6 +474,17 @@ def test_long16_kernel_vs_oracle(qlen):
     _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=qlen in (5, 400, 513, 1025, 2049), long16=1)
 
 
+@pytest.mark.parametrize("qlen", [5, 400, 513, 1025])
+def test_long16_kernel_eight_waves(qlen):
+    """long16_kernel at 8 entries (waves) per workgroup (option long16_waves,
+    one profile staged for all of them): the same scores."""
+    S.set_option("long16_waves", 8)
+    try:
+        _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1)
+    finally:
+        S.set_option("long16_waves", 4)
+
+
 @pytest.mark.parametrize("qlen", [5, 400, 1025])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
 def test_long_entry_kernel_split_launches(qlen, algo):
