@@ -115,7 +115,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "long16" 1|0         SW long entries on packed 16-bit patterns, one wave
  *                        per entry, whenever min(m, n) x max score fits (default);
  *                        0: the int32 kernel ("long_waves" applies to it)
- *   "long16_waves" 4|8   entries (waves) per long16 workgroup, sharing its profile (default 4)
+ *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
+ *                        merges at the list width k needs, for DBs of <= 256 filter blocks
+ *                        (default), or always the general scan
  *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
  *                        wave priority: none (default), one per SIMD, N
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)

@@ -815,6 +815,7 @@ static int rescore32_rl(const DeviceDB& D, size_t m, uint32_t A, int Q, int R, i
     return long_rl1(m);
 }
 constexpr uint32_t kRescoreBlocks = 1024;    // the tier's grid: 4 workgroups per CU, looping over the list
+constexpr uint32_t kTierMinBlocks = 256;     // ... or fewer when the last search's list was short
 
 // long16_kernel (SW long entries on packed 16-bit patterns): the pattern of
 // score 0 -- high enough that h + Q + R and E + R never borrow across the
@@ -1408,6 +1409,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     }
     float kms = 0, wms = 0, dms = 0;
     uint64_t wide_total = 0;
+    uint32_t tier_max = 0;           // the longest overflow list this search (DeviceDB::tier_hint)
     uint64_t kernel_bytes = 0;
     const char* kname = "";
     uint32_t srows = 0;
@@ -1687,7 +1689,12 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             ra.list_count = ovf;
             ra.list_out = wide;
             ra.nseq = (uint32_t)ovf_capv;
-            ra.blocks = (uint32_t)std::min<size_t>(kRescoreBlocks, (ovf_capv + kLongWaves - 1) / kLongWaves);
+            // grid: one workgroup per four entries of the last search's list
+            // (the list is usually empty: a full 1024-workgroup grid that only
+            // reads the count costs ~4 us), at least one per CU
+            ra.blocks = (uint32_t)std::min<size_t>(
+                std::min<size_t>(kRescoreBlocks, (ovf_capv + kLongWaves - 1) / kLongWaves),
+                std::max<size_t>(kTierMinBlocks, ((size_t)D.tier_hint + kLongWaves - 1) / kLongWaves));
             if (m > (size_t)64 * rl32) {
                 ra.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)ra.blocks * kLongWaves * ra.stride;
@@ -1817,15 +1824,13 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             if (long4 < long_groups) {
                 la.seq0 = long4 * 64;
                 la.nseq = (long_groups - long4) * 64;
-                // one entry per wave: four (or long16_waves) entries per workgroup
-                const uint32_t wpg = rl16 > 0 && C.long16_waves == 8 ? 8u : (uint32_t)kLongWaves;
-                gate_total += (la.nseq + wpg - 1) / wpg;
-                D.gate_count += (la.nseq + wpg - 1) / wpg;
+                gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
+                D.gate_count += (la.nseq + kLongWaves - 1) / kLongWaves;
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
-                    check(launch_long16(la, rl16, (int)wpg, D.stream_long1), "long kernel launch");
+                    check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
                 } else {
                     check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
                 }
@@ -2392,6 +2397,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 dst.wide[(uint64_t)key_view * E + e] = hwd[i];
             }
             wide_total += nov;
+            tier_max = std::max(tier_max, nov);
         };
         if (ind) {
             for (size_t vv = 0; vv < V; vv++) {
@@ -2536,6 +2542,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     out.wide_ms = wms;
     out.d2h_ms = dms;
     out.wide_count = wide_total;
+    D.tier_hint = tier_max;
     out.kernel_bytes = kernel_bytes;
     out.kernel = kname;
     out.strip_rows = srows;

@@ -115,6 +115,9 @@ struct DeviceDB {
     // gate_count.  cnt_dirty: zero the whole block before the next search
     // (fresh memory, or a strip part's wait-timeout word was raised)
     uint32_t gate_count = 0;
+    // the largest overflow list of the last search: sizes the re-score tier's
+    // grid (a hint only -- the tier loops over any list length)
+    uint32_t tier_hint = 0;
     bool cnt_dirty = true;
     uint32_t filter_seq = 0;              // the last FilterArgs::host_seq (never 0)
     uint32_t* d_smax = nullptr;

@@ -267,7 +267,10 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
 size_t long_lds_bytes(uint32_t alpha, int w, int rl);
 // SW long entries on packed 16-bit patterns, one wave per entry; rl (rows
 // per lane) 4, 6, 8, 10, 12 or 16, 64*rl rows per pass
-hipError_t launch_long16(const LongArgs& a, int rl, int waves, hipStream_t st);   // waves per workgroup: 4 | 8
+hipError_t launch_long16(const LongArgs& a, int rl, hipStream_t st);
+// filter_prefix with the scan states in registers for DBs of <= 256 filter
+// blocks (1, default) or always the general kernel (0; option "filter_prefix_regs")
+void set_filter_prefix_regs(int on);
 size_t long16_lds_bytes(uint32_t alpha, int rl);
 
 // The reference's 8/16-bit overflow counters (counters.hip).  m_run reports

@@ -651,22 +651,110 @@ __global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix(const FilterA
     }
 }
 
+// The same merge for lists of at most KW = 16 or 32 elements, inside aligned
+// groups of KW lanes (lanes >= K of both inputs hold INT32_MIN): the top KW of
+// the union as a bitonic sequence, max(x[i], y[KW-1-i]), then log2(KW)
+// compare-exchange stages.  KW 16 is DPP only (row_mirror reverses a row):
+// 2.5x shorter than the 64-lane merge on the scan's dependent chain.
+template <int KW>
+__device__ __forceinline__ int32_t merge_topk_w(int32_t x, int32_t y, int lane, int K) {
+    static_assert(KW == 16 || KW == 32 || KW == 64, "merge_topk_w<KW>");
+    if constexpr (KW == 64) {
+        return merge_topk(x, y, lane, K);
+    } else {
+        int32_t yr = __builtin_amdgcn_mov_dpp(y, 0x140, 0xf, 0xf, false);   // row_mirror: 15 - i in the row
+        if constexpr (KW == 32) yr = lane_xor<16>(yr, lane);                 // 31 - i in the 32
+        int32_t v = max(x, yr);
+        if constexpr (KW == 32) v = bitonic_step<16>(v, lane);
+        v = bitonic_step<8>(v, lane);
+        v = bitonic_step<4>(v, lane);
+        v = bitonic_step<2>(v, lane);
+        v = bitonic_step<1>(v, lane);
+        return lane < K ? v : INT32_MIN;
+    }
+}
+
+// filter_prefix for up to kPrefixRegs blocks per wave (nblocks <= 16 x 16 =
+// 256: a 1 M-entry shard): the wave's summaries are loaded at once and its
+// scan states stay in registers (no store and reload of FilterArgs::before),
+// and the merges run at the list width K needs.
+constexpr int kPrefixRegs = 16;
+template <int KW>
+__global__ void __launch_bounds__(64 * kPrefixWaves) filter_prefix_r(const FilterArgs a0) {
+    const FilterArgs a = filter_query(a0);
+    __shared__ int32_t carry[kPrefixWaves][64];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int K = (int)a.k;
+    const uint32_t per = (a.nblocks + kPrefixWaves - 1) / kPrefixWaves;   // <= kPrefixRegs (launch_filter)
+    const uint32_t b0 = min(a.nblocks, wave * per), nb = min(a.nblocks, b0 + per) - b0;
+    int32_t st[kPrefixRegs];
+#pragma unroll
+    for (int i = 0; i < kPrefixRegs; i++)
+        st[i] = (uint32_t)i < nb ? a.summary[(size_t)(b0 + i) * kFilterMaxK + lane] : INT32_MIN;
+    int32_t run = INT32_MIN;
+#pragma unroll
+    for (int i = 0; i < kPrefixRegs; i++) {
+        if ((uint32_t)i < nb) {
+            const int32_t blk = st[i];
+            st[i] = run;                                 // the state before block b0 + i
+            run = merge_topk_w<KW>(run, blk, lane, K);
+        }
+    }
+    // the waves' carries, as filter_prefix
+    int32_t acc = run;
+    carry[wave][lane] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int d = 1; d < kPrefixWaves; d <<= 1) {
+        const int32_t o = (int)wave >= d ? carry[wave - d][lane] : INT32_MIN;
+        __syncthreads();
+        acc = merge_topk_w<KW>(acc, o, lane, K);
+        carry[wave][lane] = acc;
+        __syncthreads();
+    }
+    const int32_t c = wave > 0 ? carry[wave - 1][lane] : INT32_MIN;
+#pragma unroll
+    for (int i = 0; i < kPrefixRegs; i++) {
+        if ((uint32_t)i < nb) {
+            const int32_t t = __builtin_amdgcn_readlane(merge_topk_w<KW>(c, st[i], lane, K), K - 1);
+            if (lane == 0) a.thresh[b0 + i] = t;
+        }
+    }
+}
+
+static int g_prefix_regs = 1;
+void set_filter_prefix_regs(int on) { g_prefix_regs = on; }
+
+// kSelectPer consecutive entries per thread (one mini, so one bound), a
+// quarter of the workgroups of one entry per thread
+constexpr uint32_t kSelectPer = 4;
 __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     const FilterArgs a = filter_query(a0);
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    if (e < a.nviews) a.counters[3 + e] = a.ovf_count[(size_t)e * a.ovf_stride];
-    if (e == 0 && a.status) a.counters[2] = *a.status;
-    if (e < a.n) {
-        const int32_t x = a.scores[a.order ? a.order[e] : e];
-        const int32_t t = max(a.thresh[e / kFilterBlock], a.thresh_local[e / kMini]);
-        if (x == INT32_MIN || x > t) {
-            const uint32_t i = atomicAdd(&a.counters[0], 1u);
-            a.cand[i] = make_uint2(e, (uint32_t)x);
-            // a merged-code entry's score is an upper bound: its exact one
-            // comes from the re-score of its lane (FilterArgs::exact_lanes)
-            if (a.emask && (a.emask[e] & a.merge_mask)) {
-                const uint32_t l = a.entry_lane[e].y;
-                if (l >= a.exact_lane0) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = l;
+    const uint32_t tid = blockIdx.x * 256 + threadIdx.x;
+    if (tid < a.nviews) a.counters[3 + tid] = a.ovf_count[(size_t)tid * a.ovf_stride];
+    if (tid == 0 && a.status) a.counters[2] = *a.status;
+    const uint32_t e0 = tid * kSelectPer;
+    if (e0 < a.n) {
+        int32_t x[kSelectPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kSelectPer; j++) {
+            const uint32_t e = e0 + j;
+            x[j] = e < a.n ? a.scores[a.order ? a.order[e] : e] : 0;
+        }
+        const int32_t t = max(a.thresh[e0 / kFilterBlock], a.thresh_local[e0 / kMini]);
+#pragma unroll
+        for (uint32_t j = 0; j < kSelectPer; j++) {
+            const uint32_t e = e0 + j;
+            if (e < a.n && (x[j] == INT32_MIN || x[j] > t)) {
+                const uint32_t i = atomicAdd(&a.counters[0], 1u);
+                a.cand[i] = make_uint2(e, (uint32_t)x[j]);
+                // a merged-code entry's score is an upper bound: its exact one
+                // comes from the re-score of its lane (FilterArgs::exact_lanes)
+                if (a.emask && (a.emask[e] & a.merge_mask)) {
+                    const uint32_t l = a.entry_lane[e].y;
+                    if (l >= a.exact_lane0) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = l;
+                }
             }
         }
     }
@@ -715,9 +803,16 @@ hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
     const uint32_t nq = a.nq > 1 ? a.nq : 1u;
     hipLaunchKernelGGL(filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+    if (g_prefix_regs && a.nblocks <= (uint32_t)(kPrefixWaves * kPrefixRegs)) {
+        if (a.k <= 16) hipLaunchKernelGGL(filter_prefix_r<16>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        else if (a.k <= 32) hipLaunchKernelGGL(filter_prefix_r<32>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        else hipLaunchKernelGGL(filter_prefix_r<64>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+    }
     if (a.host_out && (nq > 1 || !a.done)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(filter_select, dim3((a.n + 255) / 256, nq), dim3(256), 0, st, a);
+    const uint32_t sel = std::max<uint32_t>((a.n + 256 * kSelectPer - 1) / (256 * kSelectPer), (a.nviews + 255) / 256);
+    hipLaunchKernelGGL(filter_select, dim3(sel, nq), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1376,8 +1471,8 @@ struct PairSlice {
     uint32_t v[(NR + 1) & ~1];
 };
 
-template <int RL, int WV>
-__global__ void __launch_bounds__(64 * WV) long16_kernel(const LongArgs a) {
+template <int RL>
+__global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs a) {
     static_assert(RL % 2 == 0, "rows per lane come in register pairs");
     asm volatile("" ::: "v167");                     // as long_kernel: a pair wave fits where it ran
     extern __shared__ __attribute__((aligned(16))) uint32_t ptab[];   // [code][lane slot][SLW] dwords
@@ -1392,7 +1487,7 @@ __global__ void __launch_bounds__(64 * WV) long16_kernel(const LongArgs a) {
         __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t s = blockIdx.x * WV + wave;           // one entry per wave
+    const uint32_t s = blockIdx.x * kLongWaves + wave;   // one entry per wave
     const bool active = s < a.nseq;
     const uint32_t ss = a.seq0 + (active ? s : 0);
     const GroupDesc gd = a.groups[ss >> 6];
@@ -1414,7 +1509,7 @@ __global__ void __launch_bounds__(64 * WV) long16_kernel(const LongArgs a) {
         // before this pass's loads
         __threadfence();
         __syncthreads();
-        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * WV) {
+        for (uint32_t x = threadIdx.x; x < prow * CS; x += 64 * kLongWaves) {
             const uint32_t c = x / CS, rem = x % CS, sl = rem / SLW, k = rem % SLW;
             uint32_t v = padw;
             if (k < (uint32_t)NR && c < a.alpha) {
@@ -1610,39 +1705,35 @@ __global__ void __launch_bounds__(64 * WV) long16_kernel(const LongArgs a) {
 
 size_t long16_lds_bytes(uint32_t alpha, int rl) { return (size_t)(alpha + 1) * 64 * long16_slot(rl) * 4; }
 
-template <int RL, int WV>
+template <int RL>
 static hipError_t launch_long16_k(const LongArgs& a, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
     constexpr size_t kDynMax = kPairLdsMax - 8192;
     const size_t need = long16_lds_bytes(a.alpha, RL);
     if (need > kDynMax) return hipErrorInvalidValue;
     const size_t bytes = std::max<size_t>(need, std::min<size_t>(a.lds_min, kDynMax));
-    const hipError_t e = lds_attr_once((const void*)long16_kernel<RL, WV>, attr, (int)kDynMax);
+    const hipError_t e = lds_attr_once((const void*)long16_kernel<RL>, attr, (int)kDynMax);
     if (e != hipSuccess) return e;
-    const uint32_t blocks = (a.nseq + WV - 1) / WV;
-    hipLaunchKernelGGL((long16_kernel<RL, WV>), dim3(blocks), dim3(64 * WV), bytes, st, a);
+    // (four entries per workgroup: eight measured -8 % on Swiss-Prot,
+    // profiles/r05/ab/l16w8_sprot -- a finished workgroup's hole waits for
+    // its longest entry, and more prio-3 waves starve the pair waves beside them)
+    const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
+    hipLaunchKernelGGL((long16_kernel<RL>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
     return hipGetLastError();
 }
 
-template <int WV>
-static hipError_t launch_long16_w(const LongArgs& a, int rl, hipStream_t st) {
-    switch (rl) {
-        case 4: return launch_long16_k<4, WV>(a, st);
-        case 6: return launch_long16_k<6, WV>(a, st);
-        case 8: return launch_long16_k<8, WV>(a, st);
-        case 10: return launch_long16_k<10, WV>(a, st);
-        case 12: return launch_long16_k<12, WV>(a, st);
-        case 16: return launch_long16_k<16, WV>(a, st);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-hipError_t launch_long16(const LongArgs& a, int rl, int waves, hipStream_t st) {
+hipError_t launch_long16(const LongArgs& a, int rl, hipStream_t st) {
     if (a.nseq == 0) return hipSuccess;
     if (a.alpha > 32 || a.base16 < 0x0400u || a.base16 > 0x7BFFu) return hipErrorInvalidValue;
-    if (waves == 8) return launch_long16_w<8>(a, rl, st);
-    if (waves == 4) return launch_long16_w<4>(a, rl, st);
-    return hipErrorInvalidValue;
+    switch (rl) {
+        case 4: return launch_long16_k<4>(a, st);
+        case 6: return launch_long16_k<6>(a, st);
+        case 8: return launch_long16_k<8>(a, st);
+        case 10: return launch_long16_k<10>(a, st);
+        case 12: return launch_long16_k<12>(a, st);
+        case 16: return launch_long16_k<16>(a, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 // ------------------------------------------------------------------ launch

@@ -474,16 +474,6 @@ def test_long16_kernel_vs_oracle(qlen):
     _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=qlen in (5, 400, 513, 1025, 2049), long16=1)
 
 
-@pytest.mark.parametrize("qlen", [5, 400, 513, 1025])
-def test_long16_kernel_eight_waves(qlen):
-    """long16_kernel at 8 entries (waves) per workgroup (option long16_waves,
-    one profile staged for all of them): the same scores."""
-    S.set_option("long16_waves", 8)
-    try:
-        _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1)
-    finally:
-        S.set_option("long16_waves", 4)
-
 
 @pytest.mark.parametrize("qlen", [5, 400, 1025])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
@@ -1059,8 +1049,18 @@ def test_device_filter_candidate_count_is_exact(n, pattern):
                     got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
                     assert got == po.topk(exp, ids, k), (pattern, k, fh)
                     assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, fh)
+            # the block scan at every list width (filter_prefix_r<16/32/64>,
+            # k on both sides of 16 and 32) and the general scan
+            S.set_option("filter_host", 0)
+            for regs in (1, 0):
+                S.set_option("filter_prefix_regs", regs)
+                for k in (1, 10, 16, 17, 32, 33, 64):
+                    got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+                    assert got == po.topk(exp, ids, k), (pattern, k, regs)
+                    assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, regs)
         finally:
             S.set_option("filter_host", 0)
+            S.set_option("filter_prefix_regs", 1)
         S.free_sequence(qq)
 
 

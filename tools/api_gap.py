@@ -33,6 +33,13 @@ def main():
     if gaps:
         print(f"all {len(gaps)} gaps between pair launches (us): median {gaps[len(gaps) // 2]:.1f}, "
               f"min {gaps[0]:.1f}, max {gaps[-1]:.1f}")
+    durs = {}
+    for s_, e_, kind, name in ev:
+        if kind == "K":
+            durs.setdefault(name, []).append((e_ - s_) / 1e3)
+    print("kernel durations (us, median over the run):",
+          ", ".join(f"{n.split('(')[0].split('::')[-1]} {sorted(v)[len(v) // 2]:.1f}"
+                    for n, v in sorted(durs.items(), key=lambda x: -sum(x[1])) if len(v) > 2))
     a, b = pairs[gi - 1], pairs[gi]
     t0 = a[1]
     print(f"gap between pair launches ending {a[1]} and starting {b[0]}: {(b[0] - a[1]) / 1e3:.1f} us")

@@ -142,7 +142,7 @@ r5_kgap() (
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT" -o run --output-format csv \
         -- python3 "$REPO/bench.py" --steps 30 --warmup 2 --no-cpu-baseline --no-north-star "$@" > "$OUT/bench.log" 2>&1
-    python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -1 "$OUT/gap.txt"
+    python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -2 "$OUT/gap.txt"
 )
 
 "r5_$@"
