@@ -824,7 +824,44 @@ constexpr uint32_t kTierMinBlocks = 256;     // ... or fewer when the last searc
 // kernel does not apply: NW, the option off, or min(m, n) maxM (the largest
 // SW score) beyond the patterns' finite range (kernels.hip long16_kernel)
 static uint32_t long16_base(int Q, int R) { return 0x0400u + (uint32_t)std::max(0, -(Q + R)); }
-static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM) {
+static int long16_rl(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM);
+
+// long16_kernel's rows per lane RL and the query rows it leaves to its row
+// scan (LongArgs::extra16, *extra), by issue cost per DB column: a pass step
+// ~10.7 wave instructions per register (RL / 2 registers; hotloop census of
+// the 16-step body) plus kPass for a pass's ramp and profile staging, a row of
+// the scan ~1.  So q = 513 runs RL 8 + 1 scanned row instead of RL 10 with 52
+// of 64 lanes holding rows, q = 1025 one RL 16 pass + 1 row instead of two,
+// q = 1500 two RL 12 passes instead of two RL 16 ones.  Ties go to the larger
+// RL (fewer passes).
+static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM,
+                       uint32_t* extra) {
+    *extra = 0;
+    const int rl = long16_rl(D, m, nw, Q, R, minM, maxM);
+    if (rl == 0 || !cfg().long16_rows) return rl;
+    constexpr double kStep = 10.7, kRow = 1.0, kPass = 0.5;
+    constexpr size_t kExtraMax = 8;
+    double best = 1e300;
+    int brl = rl;
+    for (int r : {16, 12, 10, 8, 6, 4}) {
+        const size_t rp = (size_t)64 * r, full = m / rp, e = m - full * rp;
+        const double step = r / 2 * kStep + kPass;
+        const double c = (double)((m + rp - 1) / rp) * step;
+        if (c < best) {
+            best = c;
+            brl = r;
+            *extra = 0;
+        }
+        if (full > 0 && e > 0 && e <= kExtraMax && (double)full * step + (double)e * kRow < best) {
+            best = (double)full * step + (double)e * kRow;
+            brl = r;
+            *extra = (uint32_t)e;
+        }
+    }
+    return brl;
+}
+
+static int long16_rl(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM) {
     // (minM: a diagonal sum hd + M, hd >= base16, must stay a positive
     // pattern; a matrix value below -base16 could wrap it into the NaN
     // patterns 0xFC01..0xFFFF, which the maxima propagate)
@@ -1735,8 +1772,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             // a merge: the long entries are scored exactly on the compact codes
             // (a 35 k-residue entry re-scored by one wave would cost
             // milliseconds), so they never need the exact re-score
-            const int rl16 = merge ? long16_plan(D, m, nw, Q, R, std::min(minM, vp.xminM), std::max(maxM, vp.xmaxM))
-                                   : long16_plan(D, m, nw, Q, R, minM, maxM);
+            uint32_t extra16 = 0;
+            const int rl16 = merge ? long16_plan(D, m, nw, Q, R, std::min(minM, vp.xminM), std::max(maxM, vp.xmaxM), &extra16)
+                                   : long16_plan(D, m, nw, Q, R, minM, maxM, &extra16);
             // the longest groups on their own streams, concurrently with the
             // pair kernel (enqueued first, so their waves start first): one
             // wave per entry (RL rows per lane, 64*RL rows per pass), or --
@@ -1829,6 +1867,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
+                    la.extra16 = extra16;
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
                     check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
                 } else {
@@ -1838,7 +1877,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             if (v == 0) {
                 lentries = long_groups * 64;
-                if (rl16 > 0) snprintf(lkname, sizeof lkname, "long16_rl%d", rl16);
+                if (rl16 > 0 && extra16) snprintf(lkname, sizeof lkname, "long16_rl%d+%u", rl16, extra16);
+                else if (rl16 > 0) snprintf(lkname, sizeof lkname, "long16_rl%d", rl16);
                 else if (long4 == 0) snprintf(lkname, sizeof lkname, "long32_w1_rl%d", rl1);
                 else if (long4 == long_groups) snprintf(lkname, sizeof lkname, "long32_w4_rl%d", rl4);
                 else snprintf(lkname, sizeof lkname, "long32_w4_rl%d+w1_rl%d", rl4, rl1);

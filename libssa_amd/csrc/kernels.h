@@ -151,6 +151,11 @@ struct LongArgs {
     // long16_kernel (SW on 16-bit patterns): pattern of score 0, and the
     // padding profile value (int16 in the low half)
     uint32_t base16, pad16;
+    // long16_kernel: the query's last extra16 rows are not in any pass (m -
+    // extra16 is a whole number of 64 x RL-row passes); the wave scores them
+    // one row at a time after its passes (a prefix maximum over 64 columns
+    // per step, kernels.hip long16_rows), from the last pass's bottom row
+    uint32_t extra16;
     // long_kernel (W = 1) as the exact int32 re-score tier of the DP kernels'
     // overflowed lanes (engine.cpp): when `list` is set the entries are the
     // lanes list[0 .. min(*list_count, nseq)), in a grid of `blocks`

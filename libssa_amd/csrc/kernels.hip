@@ -1471,6 +1471,73 @@ struct PairSlice {
     uint32_t v[(NR + 1) & ~1];
 };
 
+// long16_kernel's rows past its passes (LongArgs::extra16), one row at a
+// time: the wave reads the row above -- packed (H, F) patterns per column in
+// the entry's scratch row, as a pass leaves it -- and scores 64 columns per
+// step.  Along a row of SW (R <= 0, E clamped at 0 as long16 clamps it), with
+// a(j) = max(H(r-1, j-1) + M, F(r, j), 0) and X~(j) = X(j) + (j+1)|R|:
+//   E~(j) = Q + max_{-1 <= k < j} H~(k)   (H~(-1) = 0: the zero column -1)
+//   H~(j) = max(a~(j), E~(j)),
+// and since Q <= 0, max_{k <= j} H~(k) = max_{k <= j} a~(k): the running
+// maximum of H~ is a plain prefix maximum of a~ -- the whole row in parallel
+// (a 64-lane scan per step, the previous steps' maximum carried in).
+// F(r, j) = max(F(r-1, j) + R, H(r-1, j) + Q + R, 0) is per column.  Each
+// row but the last writes its (H, F) back in place (a step reads its columns
+// before it writes them; the diagonal input of lane 0 is carried).  Returns
+// the maximum H over the rows [m0, a.m).  Values stay under long16_plan's
+// bound, so the patterns hold them.
+__device__ int32_t long16_rows(const LongArgs& a, uint32_t* scr, const uint4* rp, uint32_t n, uint32_t m0, int lane) {
+    const int32_t base = (int32_t)a.base16;
+    const int32_t Q = a.gap_open, R = a.gap_extend, Rabs = -R;
+    const uint32_t padc = a.alpha;
+    int32_t best = 0;
+    for (uint32_t r = m0; r < a.m; r++) {
+        const uint32_t qr = a.query[r];
+        const bool feeds = r + 1 < a.m;
+        int32_t carry_m = 0;                          // max of H~ over the columns so far (H~(-1) = 0)
+        int32_t carry_h = 0;                          // H(r-1, c0-1): the diagonal input of lane 0
+        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+            const uint32_t j = c0 + (uint32_t)lane;
+            const bool valid = j < n;
+            const uint32_t pk = valid ? __hip_atomic_load(scr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : (uint32_t)base * 0x10001u;
+            const int32_t hu = (int32_t)(pk & 0xffffu) - base, fu = (int32_t)(pk >> 16) - base;
+            int32_t hd = __shfl_up(hu, 1);
+            if (lane == 0) hd = carry_h;
+            carry_h = __builtin_amdgcn_readlane(hu, 63);
+            uint32_t code = padc;
+            if (valid) {
+                const uint4 v = rp[(size_t)(j >> 4) * 64];
+                const uint32_t q4 = (j >> 2) & 3;
+                const uint32_t w = q4 == 0 ? v.x : q4 == 1 ? v.y : q4 == 2 ? v.z : v.w;
+                code = (w >> (8 * (j & 3))) & 0xffu;
+            }
+            const int32_t f = max(max(fu + R, hu + Q + R), 0);
+            const int32_t av = max(max(hd + (int32_t)a.matrix[(code << 5) + qr], f), 0);
+            const int32_t off = (int32_t)(j + 1) * Rabs;
+            const int32_t at = valid ? av + off : INT32_MIN / 2;
+            int32_t pm = at;                          // inclusive prefix maximum over the lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(pm, o);
+                if (lane >= o) pm = max(pm, y);
+            }
+            int32_t ex = __shfl_up(pm, 1);
+            ex = lane == 0 ? carry_m : max(carry_m, ex);
+            carry_m = max(carry_m, __builtin_amdgcn_readlane(pm, 63));
+            const int32_t h = max(at, Q + ex) - off;
+            if (valid) {
+                best = max(best, h);
+                if (feeds)
+                    __hip_atomic_store(scr + j, (uint32_t)(h + base) | ((uint32_t)(f + base) << 16), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    for (int x = 32; x > 0; x >>= 1) best = max(best, __shfl_xor(best, x));
+    return best;
+}
+
 template <int RL>
 __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs a) {
     static_assert(RL % 2 == 0, "rows per lane come in register pairs");
@@ -1497,7 +1564,9 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
     const uint32_t BP = a.base16 * 0x10001u;
     const int32_t QR = a.gap_open + a.gap_extend, R = a.gap_extend;
     const uint32_t cQR = (uint32_t)(QR * 65536 + QR), cR = (uint32_t)(R * 65536 + R);
-    const uint32_t m = a.m, prow = a.alpha + 1, padc = a.alpha;
+    // the passes cover the first m - extra16 rows (a multiple of RP when
+    // extra16 > 0), long16_rows the rest
+    const uint32_t m = a.m - a.extra16, prow = a.alpha + 1, padc = a.alpha;
     const uint32_t padw = (a.pad16 & 0xffffu) * 0x10001u;
     const uint32_t npass = (m + RP - 1) / RP;
     uint32_t S = BP;
@@ -1576,7 +1645,7 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
             return c < n ? __hip_atomic_load(scr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : BP;
         };
         const bool from_scr = p > 0;
-        const bool feeds_scratch = !lastp;
+        const bool feeds_scratch = !lastp || a.extra16 > 0;
         uint32_t row = BP, row_next = BP;
         PairSlice<NR> pq0, pq1;
         if (from_scr) {
@@ -1695,9 +1764,14 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
     // patterns order as integers (all >= base16)
     uint32_t smax = max(S & 0xffffu, S >> 16);
     for (int x = 32; x > 0; x >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, x));
+    int32_t score = (int32_t)smax - (int32_t)a.base16;
+    if (a.extra16 && active && n > 0) {
+        __threadfence();                             // the last pass's scratch row, visible to every lane
+        score = max(score, long16_rows(a, scr, rp, n, m, lane));
+    }
     if (active && lane == 0) {
         const uint32_t o = a.lane_out[ss];
-        if (o != 0xffffffffu) a.scores[o] = (int32_t)smax - (int32_t)a.base16;
+        if (o != 0xffffffffu) a.scores[o] = score;
     }
     if (a.timeline && active && lane == 0)
         a.timeline[ss] = make_uint4(0x80000000u | ss, t_start, (uint32_t)__builtin_amdgcn_s_memrealtime(), hw_place());

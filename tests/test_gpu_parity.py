@@ -275,7 +275,7 @@ def test_query_length_edges_vs_oracle(qlen, algo):
         S.free_sequence(qq)
 
 
-def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0):
+def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0, kernel=None):
     rng = np.random.default_rng(1000 + qlen)
     q = syn.protein_query(qlen, 200 + qlen)
     head = [3000, 1, 0, 2500, 17, 64, 4100, qlen + 7] + ([35000, 22000, 20001] if huge else [])
@@ -311,6 +311,7 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0):
                     if lg:
                         packed = long16 and algo == S.SW
                         assert st["long_kernel"].startswith("long16" if packed else "long32"), st["long_kernel"]
+                        assert kernel is None or st["long_kernel"] == kernel, (st["long_kernel"], kernel)
                 got = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
                 assert got == po.topk(exp, keep.astype(np.uint64), 10)
         finally:
@@ -473,6 +474,24 @@ def test_long16_kernel_vs_oracle(qlen):
     the query lengths the benchmark configurations use."""
     _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=qlen in (5, 400, 513, 1025, 2049), long16=1)
 
+
+
+@pytest.mark.parametrize("qlen", [262, 520, 1032, 2056])
+@pytest.mark.parametrize("rows", [1, 0])
+def test_long16_row_scan(qlen, rows):
+    """long16_kernel's row scan (LongArgs::extra16): whole passes of fewer
+    rows per lane plus 6-8 query rows scored one row at a time by a prefix
+    maximum over 64 columns per step (q = 262: RL 4 + 6, 520: RL 8 + 8, 1032
+    and 2056: RL 16 passes + 8), and the same lengths without it (option
+    long16_rows 0: RL 6 / 10 single passes, two and three RL 16 passes) --
+    every score the oracle's, with the 20-35 k-residue entries."""
+    plan = {262: ("long16_rl4+6", "long16_rl6"), 520: ("long16_rl8+8", "long16_rl10"),
+            1032: ("long16_rl16+8", "long16_rl16"), 2056: ("long16_rl16+8", "long16_rl16")}[qlen]
+    S.set_option("long16_rows", rows)
+    try:
+        _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1, kernel=plan[0] if rows else plan[1])
+    finally:
+        S.set_option("long16_rows", 1)
 
 
 @pytest.mark.parametrize("qlen", [5, 400, 1025])
