@@ -102,6 +102,10 @@ void DeviceDB::release() {
     for (auto& e : vev) (void)hipEventDestroy(e);
     vev.clear();
     d_top = nullptr;
+    dfree(d_topc);
+    d_topc = nullptr;
+    topc_cap = 0;
+    topc_key = ~0ull;
     dfree(d_fbuf); dfree(d_summary); dfree(d_before); dfree(d_thresh); dfree(d_thresh_local);
     if (h_fbuf) (void)hipHostFree(h_fbuf);
     if (h_up) (void)hipHostFree(h_up);
@@ -1567,10 +1571,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // 0), diagonal-relative patterns, one dword per column up to the
         // longest group's ncols (kernels.h StripArgs::top)
         std::vector<uint32_t> top;
+        const bool top_cached = use_pair && !nw && !fused;
         if (use_pair) {
             const size_t ncols_max = ((size_t)(D.len_sorted.empty() ? 0 : D.len_sorted.back()) + 1 + 3) & ~(size_t)3;
-            top.resize(std::max<size_t>(ncols_max, 4));
-            if (nw) {
+            const uint64_t tkey = (uint64_t)(uint32_t)R << 32 ^ (uint64_t)ncols_max;
+            // (cached and current: nothing to build or upload)
+            if (!top_cached || D.topc_key != tkey) top.resize(std::max<size_t>(ncols_max, 4));
+            if (top.empty()) {
+            } else if (nw) {
                 auto pat = [&](int v) { return (uint32_t)(v + (int)nw_base) & 0xffffu; };
                 std::fill(top.begin(), top.end(), pat(Q + 2 * R) | (pat(2 * Q + 2 * R) << 16));
             } else {
@@ -1581,6 +1589,19 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     t = v;
                     v += rabs * 0x10001u;
                 }
+            }
+            if (top_cached && !top.empty()) {
+                // (every search before this one has drained the stream; the
+                // views of one search share the key)
+                if (D.topc_cap < top.size()) {
+                    check(hipStreamSynchronize(st), "sync");
+                    dfree(D.d_topc);
+                    check(hipMalloc((void**)&D.d_topc, (top.size() + 4) * 4), "first-strip boundary");
+                    D.topc_cap = top.size() + 4;
+                }
+                check(hipMemcpy(D.d_topc, top.data(), top.size() * 4, hipMemcpyHostToDevice), "H2D boundary");
+                D.topc_key = tkey;
+                top.clear();
             }
         }
         // device upload block: [matrix 8 KB][top boundary][query codes]
@@ -1624,7 +1645,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             dqpt = D.d_qpt;
         }
         D.d_matrix = (int64_t*)dup;
-        D.d_top = (uint32_t*)(dup + kUpHeader);
+        D.d_top = top_cached ? D.d_topc : (uint32_t*)(dup + kUpHeader);
         D.d_query = dup + kUpHeader + top_bytes;
         // staging mirrors the device block, then the strip kernels' table
         uint8_t* up_m = hup;

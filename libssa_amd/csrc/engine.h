@@ -76,6 +76,12 @@ struct DeviceDB {
     uint8_t* d_upblk = nullptr;
     size_t upblk_cap = 0;
     uint32_t* d_top = nullptr;
+    // SW's first-strip boundary depends only on R and the longest group: kept
+    // on the device (d_topc, key topc_key) instead of built and uploaded per
+    // search (140 KB for a 35 k-residue entry); d_top then points here
+    uint32_t* d_topc = nullptr;
+    size_t topc_cap = 0;
+    uint64_t topc_key = ~0ull;
     uint8_t* d_query = nullptr;
     int64_t* d_matrix = nullptr;
     int64_t* d_work = nullptr;
