@@ -8,8 +8,9 @@ set -o pipefail
 r5_tests() (
     # the GPU parity suite (optionally -k filter as $1)
     mkdir -p gpurun_out/r5
-    K=${1:+-k "$1"}
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread $K \
+    K=()
+    [ -n "$1" ] && K=(-k "$1")
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${K[@]}" \
         > gpurun_out/r5/gpu_tests.log 2>&1 || { tail -40 gpurun_out/r5/gpu_tests.log; exit 1; }
     tail -3 gpurun_out/r5/gpu_tests.log
 )
@@ -143,6 +144,18 @@ r5_kgap() (
     timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT" -o run --output-format csv \
         -- python3 "$REPO/bench.py" --steps 30 --warmup 2 --no-cpu-baseline --no-north-star "$@" > "$OUT/bench.log" 2>&1
     python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -2 "$OUT/gap.txt"
+)
+
+r5_final() (
+    # the default bench line (python bench.py: C2 headline, north_star,
+    # cpu_baseline) under rocprofv3 --kernel-trace --stats: the summary whose
+    # pair-kernel average the line's roofline must agree with
+    OUT=$(realpath -m gpurun_out/r5/final); mkdir -p "$OUT"
+    REPO=$PWD
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+        -- python3 "$REPO/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+    tail -1 "$OUT/bench.json" | cut -c1-400
 )
 
 "r5_$@"
