@@ -1473,17 +1473,18 @@ struct PairSlice {
 
 // long16_kernel's rows past its passes (LongArgs::extra16), one row at a
 // time: the wave reads the row above -- packed (H, F) patterns per column in
-// the entry's scratch row, as a pass leaves it -- and scores 64 columns per
-// step.  Along a row of SW (R <= 0, E clamped at 0 as long16 clamps it), with
-// a(j) = max(H(r-1, j-1) + M, F(r, j), 0) and X~(j) = X(j) + (j+1)|R|:
+// the entry's scratch row, as a pass leaves it: H of row r-1 and F into row
+// r -- and scores 64 columns per step.  Along a row of SW (R <= 0, E clamped
+// at 0 as long16 clamps it), with a(j) = max(H(r-1, j-1) + M, F(r, j), 0) and
+// X~(j) = X(j) + (j+1)|R|:
 //   E~(j) = Q + max_{-1 <= k < j} H~(k)   (H~(-1) = 0: the zero column -1)
 //   H~(j) = max(a~(j), E~(j)),
 // and since Q <= 0, max_{k <= j} H~(k) = max_{k <= j} a~(k): the running
 // maximum of H~ is a plain prefix maximum of a~ -- the whole row in parallel
 // (a 64-lane scan per step, the previous steps' maximum carried in).
-// F(r, j) = max(F(r-1, j) + R, H(r-1, j) + Q + R, 0) is per column.  Each
-// row but the last writes its (H, F) back in place (a step reads its columns
-// before it writes them; the diagonal input of lane 0 is carried).  Returns
+// Each row but the last writes back, in place, its H and the F into the next
+// row, max(F(r, j) + R, H(r, j) + Q + R, 0) (a step reads its columns before it
+// writes them; the diagonal input of lane 0 is carried).  Returns
 // the maximum H over the rows [m0, a.m).  Values stay under long16_plan's
 // bound, so the patterns hold them.
 __device__ int32_t long16_rows(const LongArgs& a, uint32_t* scr, const uint4* rp, uint32_t n, uint32_t m0, int lane) {
@@ -1512,8 +1513,8 @@ __device__ int32_t long16_rows(const LongArgs& a, uint32_t* scr, const uint4* rp
                 const uint32_t w = q4 == 0 ? v.x : q4 == 1 ? v.y : q4 == 2 ? v.z : v.w;
                 code = (w >> (8 * (j & 3))) & 0xffu;
             }
-            const int32_t f = max(max(fu + R, hu + Q + R), 0);
-            const int32_t av = max(max(hd + (int32_t)a.matrix[(code << 5) + qr], f), 0);
+            // (the scratch row carries F into row r, as a pass leaves it)
+            const int32_t av = max(max(hd + (int32_t)a.matrix[(code << 5) + qr], fu), 0);
             const int32_t off = (int32_t)(j + 1) * Rabs;
             const int32_t at = valid ? av + off : INT32_MIN / 2;
             int32_t pm = at;                          // inclusive prefix maximum over the lanes
@@ -1528,9 +1529,11 @@ __device__ int32_t long16_rows(const LongArgs& a, uint32_t* scr, const uint4* rp
             const int32_t h = max(at, Q + ex) - off;
             if (valid) {
                 best = max(best, h);
-                if (feeds)
-                    __hip_atomic_store(scr + j, (uint32_t)(h + base) | ((uint32_t)(f + base) << 16), __ATOMIC_RELAXED,
+                if (feeds) {
+                    const int32_t fn = max(max(fu + R, h + Q + R), 0);          // F into row r + 1
+                    __hip_atomic_store(scr + j, (uint32_t)(h + base) | ((uint32_t)(fn + base) << 16), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
