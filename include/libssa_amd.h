@@ -118,8 +118,10 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
  *                        merges at the list width k needs, for DBs of <= 256 filter blocks
  *                        (default), or always the general scan
- *   "long16_rows" 1|0    long16 may score up to 8 last query rows with a row scan after whole
- *                        passes of fewer rows per lane when that issues less (default 1)
+ *   "long_gate" 1|0      the pair kernel starts after the long-entry workgroups have (default 1;
+ *                        0: no wait, the long-entry streams' priority alone orders them)
+ *   "long16_rows" 1|0    queries beyond 1 024 rows: long16 passes planned by issue cost, up to 8
+ *                        last rows scored by a row scan (default 1); 0: RL 16 passes
  *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
  *                        wave priority: none (default), one per SIMD, N
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)

@@ -398,8 +398,16 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         // made first keeps its flags (the call's error is cleared)
         if (C.sync_spin && hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
-        check(hipStreamCreateWithFlags(&D.stream_long, hipStreamNonBlocking), "hipStreamCreate");
-        check(hipStreamCreateWithFlags(&D.stream_long1, hipStreamNonBlocking), "hipStreamCreate");
+        // the long-entry kernels' streams at the device's highest priority:
+        // their workgroups are the search's critical path (see also the gate,
+        // TableArgs::gate)
+        int prio_lo = 0, prio_hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) {
+            (void)hipGetLastError();
+            prio_hi = 0;
+        }
+        check(hipStreamCreateWithPriority(&D.stream_long, hipStreamNonBlocking, prio_hi), "hipStreamCreate");
+        check(hipStreamCreateWithPriority(&D.stream_long1, hipStreamNonBlocking, prio_hi), "hipStreamCreate");
         for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -831,25 +839,29 @@ static uint32_t long16_base(int Q, int R) { return 0x0400u + (uint32_t)std::max(
 static int long16_rl(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM);
 
 // long16_kernel's rows per lane RL and the query rows it leaves to its row
-// scan (LongArgs::extra16, *extra), by issue cost per DB column: a pass step
-// ~10.7 wave instructions per register (RL / 2 registers; hotloop census of
-// the 16-step body) plus kPass for a pass's ramp and profile staging, a row of
-// the scan ~1.  So q = 513 runs RL 8 + 1 scanned row instead of RL 10 with 52
-// of 64 lanes holding rows, q = 1025 one RL 16 pass + 1 row instead of two,
-// q = 1500 two RL 12 passes instead of two RL 16 ones.  Ties go to the larger
-// RL (fewer passes).
+// scan (LongArgs::extra16, *extra).  Up to 1 024 rows: the smallest RL that
+// holds the query in one pass (q = 513 at RL 8 + 1 scanned row instead of RL
+// 10 issues 18 % less but measured no faster on the Swiss-Prot form,
+// profiles/r05/ab/rows_sprot: the long waves' issue is not what the search
+// waits on there).  Beyond, by issue cost per DB column: a pass step ~10.7 wave
+// instructions per register (RL / 2 registers; hotloop census of the 16-step
+// body) plus kPass for a pass's ramp and profile staging, a scanned row ~1 --
+// q = 1025 one RL 16 pass + 1 row instead of two passes, q = 1500 two RL 12
+// passes instead of two RL 16 ones (RL >= 8).  Ties go to the larger RL.
 static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t minM, int64_t maxM,
                        uint32_t* extra) {
     *extra = 0;
     const int rl = long16_rl(D, m, nw, Q, R, minM, maxM);
-    if (rl == 0 || !cfg().long16_rows) return rl;
-    constexpr double kStep = 10.7, kRow = 1.0, kPass = 0.5;
+    if (rl == 0 || !cfg().long16_rows || m <= (size_t)64 * 16) return rl;
+    // (a pass's ramp, 2 x 63 steps, and profile staging: ~5 % of its steps
+    // on a long entry; RL >= 8 keeps the pass count low)
+    constexpr double kStep = 10.7, kRow = 1.0, kRamp = 1.05;
     constexpr size_t kExtraMax = 8;
     double best = 1e300;
     int brl = rl;
-    for (int r : {16, 12, 10, 8, 6, 4}) {
+    for (int r : {16, 12, 10, 8}) {
         const size_t rp = (size_t)64 * r, full = m / rp, e = m - full * rp;
-        const double step = r / 2 * kStep + kPass;
+        const double step = r / 2 * kStep * kRamp;
         const double c = (double)((m + rp - 1) / rp) * step;
         if (c < best) {
             best = c;
@@ -1935,7 +1947,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 if (C.pair_ticket || (!no_parts && strip_parts(T) > 1)) ta.zero_ticket = gate + 1;
             }
-            if (long_groups > 0) {
+            if (long_groups > 0 && C.long_gate) {
                 // (at most what can be resident at once: every long workgroup
                 // pads its LDS to the pair table's size, so a CU holds
                 // floor(160 KiB / that) of them -- beyond it the target is

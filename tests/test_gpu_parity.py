@@ -476,17 +476,17 @@ def test_long16_kernel_vs_oracle(qlen):
 
 
 
-@pytest.mark.parametrize("qlen", [262, 520, 1032, 2056])
+@pytest.mark.parametrize("qlen", [1025, 1032, 1500, 2056])
 @pytest.mark.parametrize("rows", [1, 0])
 def test_long16_row_scan(qlen, rows):
-    """long16_kernel's row scan (LongArgs::extra16): whole passes of fewer
-    rows per lane plus 6-8 query rows scored one row at a time by a prefix
-    maximum over 64 columns per step (q = 262: RL 4 + 6, 520: RL 8 + 8, 1032
-    and 2056: RL 16 passes + 8), and the same lengths without it (option
-    long16_rows 0: RL 6 / 10 single passes, two and three RL 16 passes) --
-    every score the oracle's, with the 20-35 k-residue entries."""
-    plan = {262: ("long16_rl4+6", "long16_rl6"), 520: ("long16_rl8+8", "long16_rl10"),
-            1032: ("long16_rl16+8", "long16_rl16"), 2056: ("long16_rl16+8", "long16_rl16")}[qlen]
+    """long16_kernel beyond 1 024 query rows (long16_plan): whole passes plus
+    1-8 query rows scored one row at a time by a prefix maximum over 64 columns
+    per step (q = 1025 / 1032: one RL 16 pass + 1 / 8 rows, 2056: two + 8),
+    two RL 12 passes for q = 1500, and the same lengths without the plan
+    (option long16_rows 0: RL 16 passes) -- every score the oracle's, with
+    the 20-35 k-residue entries."""
+    plan = {1025: ("long16_rl16+1", "long16_rl16"), 1032: ("long16_rl16+8", "long16_rl16"),
+            1500: ("long16_rl12", "long16_rl16"), 2056: ("long16_rl16+8", "long16_rl16")}[qlen]
     S.set_option("long16_rows", rows)
     try:
         _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1, kernel=plan[0] if rows else plan[1])
