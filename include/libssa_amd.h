@@ -118,6 +118,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
  *                        merges at the list width k needs, for DBs of <= 256 filter blocks
  *                        (default), or always the general scan
+ *   "tier_defer" 1|0     single-view searches: the exact re-score tier runs only when the device
+ *                        filter's header reports overflowed lanes, after the result's copy
+ *                        (default 1); 0: always, between the DP kernels and the filter
  *   "long_gate" 1|0      the pair kernel starts after the long-entry workgroups have (default 1;
  *                        0: no wait, the long-entry streams' priority alone orders them)
  *   "long16_rows" 1|0    queries beyond 1 024 rows: long16 passes planned by issue cost, up to 8

@@ -1743,6 +1743,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // output, so the tier leaves the path from the pair kernel's end to
         // the result; the tables kernel then clears the filter header
         const bool side_tier = C.side_tier && rl32 > 0 && use_pair && out.sparse && !piped && !want_counts;
+        // ... or after it, only when the search has overflowed lanes: the
+        // filter forwards every overflowed lane (INT32_MIN) and leaves it out
+        // of its bounds, so the tier's exact scores are needed only by the
+        // host, which sees the list's length in the candidate header -- the
+        // usual search (no overflow) then skips the tier's launch (~5 us on
+        // the path from the pair kernel to the result, profiles/r05/host_gap)
+        const bool defer_tier = C.tier_defer && !side_tier && rl32 > 0 && use_pair && out.sparse && !piped &&
+                                !want_counts && !merge;
         LongArgs ra{};
         if (rl32 > 0) {
             ra.res = dres;
@@ -1937,7 +1945,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             ta.rel = rel;
             ta.pad = (uint32_t)(uint16_t)padv;
             ta.zero = ovf;
-            if (side_tier) {
+            if (side_tier || defer_tier) {
                 ta.zero_hdr = D.d_fbuf;
                 ta.nzero_hdr = kFilterHeader;
             }
@@ -2138,6 +2146,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 check(hipStreamWaitEvent(D.stream_long1, ev_k1, 0), "event wait");
                 check(launch_long(ra, 1, rl32, nw, D.stream_long1), "int32 re-score launch");
                 check(hipEventRecord(D.ev[8], D.stream_long1), "event");
+            } else if (defer_tier) {
+                // (after the result's copy, if the header reports overflowed lanes)
             } else if (rl32 > 0) {
                 // the int32 tier clears what wide_kernel would have (one launch)
                 LongArgs rz = ra;
@@ -2526,6 +2536,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 for (uint32_t i = 0; i < nc; i++) out.cand[i] = D.h_order[out.cand[i]];
             for (size_t vv = 0; vv < (multi ? V : 1); vv++) {
                 const uint32_t nov = D.h_fbuf[3 + vv];
+                if (nov && defer_tier) {
+                    check(launch_long(ra, 1, rl32, nw, st), "int32 re-score launch");
+                    check(hipStreamSynchronize(st), "re-score");
+                }
                 if (nov) take_wide(multi ? vv : v, nov, out, multi ? vv : v);
             }
             if (merge) {

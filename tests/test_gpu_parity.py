@@ -683,8 +683,18 @@ def test_int16_overflow_reroute(algo):
                 assert (sc == exp).all(), lg
                 if lg == 0:
                     assert S.stats()["wide_count"] >= 1
+                # through the device filter (k <= 64): the int32 tier after the
+                # result's copy when the header reports overflowed lanes
+                # (option tier_defer, default) or before the filter
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                ids = np.arange(4, dtype=np.uint64)
+                for td in (1, 0):
+                    S.set_option("tier_defer", td)
+                    for k in (1, 3):
+                        assert [(h["score"], h["id"]) for h in fn(qq, k, 16)] == po.topk(exp, ids, k), (lg, td, k)
         finally:
             S.set_option("long_groups", -1)
+            S.set_option("tier_defer", 1)
         S.free_sequence(qq)
 
 
