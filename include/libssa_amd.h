@@ -123,8 +123,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        (default 1); 0: always, between the DP kernels and the filter
  *   "long_gate" 1|0      the pair kernel starts after the long-entry workgroups have (default 1;
  *                        0: no wait, the long-entry streams' priority alone orders them)
- *   "long16_rows" 1|0    queries beyond 1 024 rows: long16 passes planned by issue cost, up to 8
- *                        last rows scored by a row scan (default 1); 0: RL 16 passes
+ *   "long16_rows" 1|0|2  queries beyond 1 024 rows: long16 passes planned by issue cost, up to 8
+ *                        last rows scored by a row scan (default 1); 0: RL 16 passes; 2: the
+ *                        cost model at every query length (q = 513: RL 8 + 1 scanned row)
  *   "pair_prio_groups" 0|-1|N  pair-kernel groups (longest first) at raised
  *                        wave priority: none (default), one per SIMD, N
  *   "timeline" 0|1       1: record every DP wave's start/end (ssa_amd_get_timeline)

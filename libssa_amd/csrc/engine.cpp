@@ -852,14 +852,15 @@ static int long16_plan(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64
                        uint32_t* extra) {
     *extra = 0;
     const int rl = long16_rl(D, m, nw, Q, R, minM, maxM);
-    if (rl == 0 || !cfg().long16_rows || m <= (size_t)64 * 16) return rl;
+    if (rl == 0 || !cfg().long16_rows || (m <= (size_t)64 * 16 && cfg().long16_rows != 2)) return rl;
     // (a pass's ramp, 2 x 63 steps, and profile staging: ~5 % of its steps
     // on a long entry; RL >= 8 keeps the pass count low)
     constexpr double kStep = 10.7, kRow = 1.0, kRamp = 1.05;
     constexpr size_t kExtraMax = 8;
     double best = 1e300;
     int brl = rl;
-    for (int r : {16, 12, 10, 8}) {
+    for (int r : {16, 12, 10, 8, 6, 4}) {
+        if (r < 8 && m > (size_t)64 * 16) continue;
         const size_t rp = (size_t)64 * r, full = m / rp, e = m - full * rp;
         const double step = r / 2 * kStep * kRamp;
         const double c = (double)((m + rp - 1) / rp) * step;

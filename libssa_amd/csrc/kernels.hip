@@ -1487,44 +1487,65 @@ struct PairSlice {
 // writes them; the diagonal input of lane 0 is carried).  Returns
 // the maximum H over the rows [m0, a.m).  Values stay under long16_plan's
 // bound, so the patterns hold them.
+// (a step is latency-bound -- one wave, dependent lane moves -- so its lane
+// moves are DPP, not the LDS crossbar: the inclusive prefix maximum in six
+// GFX9 DPP steps (row_shr 1/2/4/8, row_bcast 15/31), the shifts by one lane
+// wave_shr:1; the matrix row of r's residue sits in one VGPR (lane c holds
+// M[c][q_r]); the next step's scratch and residue loads are issued a step ahead)
+__device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
+    constexpr int32_t I = INT32_MIN;
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x142, 0xa, 0xf, false));   // row_bcast:15 (rows 1, 3)
+    x = max(x, __builtin_amdgcn_update_dpp(I, x, 0x143, 0xc, 0xf, false));   // row_bcast:31 (rows 2, 3)
+    return x;
+}
+__device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t lane0) {
+    return __builtin_amdgcn_update_dpp(lane0, x, 0x138, 0xf, 0xf, false);    // wave_shr:1, lane 0 <- lane0
+}
 __device__ int32_t long16_rows(const LongArgs& a, uint32_t* scr, const uint4* rp, uint32_t n, uint32_t m0, int lane) {
     const int32_t base = (int32_t)a.base16;
     const int32_t Q = a.gap_open, R = a.gap_extend, Rabs = -R;
     const uint32_t padc = a.alpha;
+    const uint32_t pk_pad = (uint32_t)base * 0x10001u;
+    auto load_pk = [&](uint32_t j) -> uint32_t {
+        return j < n ? __hip_atomic_load(scr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pk_pad;
+    };
+    auto load_res = [&](uint32_t j) -> uint4 { return j < n ? rp[(size_t)(j >> 4) * 64] : make_uint4(0, 0, 0, 0); };
     int32_t best = 0;
     for (uint32_t r = m0; r < a.m; r++) {
+        // (the previous row's stores before this row's loads of the same words)
+        if (r > m0) __threadfence();
         const uint32_t qr = a.query[r];
         const bool feeds = r + 1 < a.m;
+        // lane c: M[c][q_r] (c < 32; the padding code's row too)
+        const int32_t mrow = lane < 32 ? (int32_t)a.matrix[((uint32_t)lane << 5) + qr] : 0;
         int32_t carry_m = 0;                          // max of H~ over the columns so far (H~(-1) = 0)
         int32_t carry_h = 0;                          // H(r-1, c0-1): the diagonal input of lane 0
+        uint32_t pk_n = load_pk((uint32_t)lane);
+        uint4 v_n = load_res((uint32_t)lane);
         for (uint32_t c0 = 0; c0 < n; c0 += 64) {
             const uint32_t j = c0 + (uint32_t)lane;
             const bool valid = j < n;
-            const uint32_t pk = valid ? __hip_atomic_load(scr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : (uint32_t)base * 0x10001u;
+            const uint32_t pk = pk_n;
+            const uint4 v = v_n;
+            pk_n = load_pk(j + 64);
+            v_n = load_res(j + 64);
             const int32_t hu = (int32_t)(pk & 0xffffu) - base, fu = (int32_t)(pk >> 16) - base;
-            int32_t hd = __shfl_up(hu, 1);
-            if (lane == 0) hd = carry_h;
+            const int32_t hd = wave_shr1(hu, carry_h);
             carry_h = __builtin_amdgcn_readlane(hu, 63);
-            uint32_t code = padc;
-            if (valid) {
-                const uint4 v = rp[(size_t)(j >> 4) * 64];
-                const uint32_t q4 = (j >> 2) & 3;
-                const uint32_t w = q4 == 0 ? v.x : q4 == 1 ? v.y : q4 == 2 ? v.z : v.w;
-                code = (w >> (8 * (j & 3))) & 0xffu;
-            }
+            const uint32_t q4 = (j >> 2) & 3;
+            const uint32_t w = q4 == 0 ? v.x : q4 == 1 ? v.y : q4 == 2 ? v.z : v.w;
+            const uint32_t code = valid ? (w >> (8 * (j & 3))) & 0xffu : padc;
+            const int32_t sc = __builtin_amdgcn_ds_bpermute((int)(code << 2), mrow);
             // (the scratch row carries F into row r, as a pass leaves it)
-            const int32_t av = max(max(hd + (int32_t)a.matrix[(code << 5) + qr], fu), 0);
+            const int32_t av = max(max(hd + sc, fu), 0);
             const int32_t off = (int32_t)(j + 1) * Rabs;
             const int32_t at = valid ? av + off : INT32_MIN / 2;
-            int32_t pm = at;                          // inclusive prefix maximum over the lanes
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(pm, o);
-                if (lane >= o) pm = max(pm, y);
-            }
-            int32_t ex = __shfl_up(pm, 1);
-            ex = lane == 0 ? carry_m : max(carry_m, ex);
+            const int32_t pm = wave_prefix_max(at);   // inclusive prefix maximum over the lanes
+            const int32_t ex = max(carry_m, wave_shr1(pm, INT32_MIN));
             carry_m = max(carry_m, __builtin_amdgcn_readlane(pm, 63));
             const int32_t h = max(at, Q + ex) - off;
             if (valid) {

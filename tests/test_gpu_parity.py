@@ -476,8 +476,8 @@ def test_long16_kernel_vs_oracle(qlen):
 
 
 
-@pytest.mark.parametrize("qlen", [1025, 1032, 1500, 2056])
-@pytest.mark.parametrize("rows", [1, 0])
+@pytest.mark.parametrize("qlen", [1025, 1032, 1500, 2056, 262, 513])
+@pytest.mark.parametrize("rows", [1, 0, 2])
 def test_long16_row_scan(qlen, rows):
     """long16_kernel beyond 1 024 query rows (long16_plan): whole passes plus
     1-8 query rows scored one row at a time by a prefix maximum over 64 columns
@@ -485,11 +485,16 @@ def test_long16_row_scan(qlen, rows):
     two RL 12 passes for q = 1500, and the same lengths without the plan
     (option long16_rows 0: RL 16 passes) -- every score the oracle's, with
     the 20-35 k-residue entries."""
-    plan = {1025: ("long16_rl16+1", "long16_rl16"), 1032: ("long16_rl16+8", "long16_rl16"),
-            1500: ("long16_rl12", "long16_rl16"), 2056: ("long16_rl16+8", "long16_rl16")}[qlen]
+    # (option 2: the cost model below 1 024 rows too -- q = 262: RL 4 + 6, 513: RL 8 + 1)
+    plan = {1025: ("long16_rl16+1", "long16_rl16", "long16_rl16+1"),
+            1032: ("long16_rl16+8", "long16_rl16", "long16_rl16+8"),
+            1500: ("long16_rl12", "long16_rl16", "long16_rl12"),
+            2056: ("long16_rl16+8", "long16_rl16", "long16_rl16+8"),
+            262: ("long16_rl6", "long16_rl6", "long16_rl4+6"),
+            513: ("long16_rl10", "long16_rl10", "long16_rl8+1")}[qlen]
     S.set_option("long16_rows", rows)
     try:
-        _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1, kernel=plan[0] if rows else plan[1])
+        _long_entry_case(qlen, S.SW, (-11, -1), 1, huge=True, long16=1, kernel=plan[{1: 0, 0: 1, 2: 2}[rows]])
     finally:
         S.set_option("long16_rows", 1)
 
