@@ -76,10 +76,12 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # pair-row stream; SW 6.444e9 x 64 / 1.406e11 = 2.93, NW 80-row 1.439e10 x
 # 64 / 3.516e11 = 2.62) and round 4 (16-bit pair-row stream: profiles/r04/
 # pmc_final/c2 SW 6.489e9 x 64 / 1.406e11 = 2.95, profiles/r04/pmc/c3 NW
-# 1.435e10 x 64 / 3.516e11 = 2.61).  Keyed by (kernel, pair strip rows): the
-# instruction count per cell depends on the strip height.
-VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 2.95,
-                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.61}
+# 1.435e10 x 64 / 3.516e11 = 2.61) and round 5 (row-drop table, SW floors in
+# one SGPR: profiles/r05/pmc_final2/c2 2.962, profiles/r05/pmc_final/c3 2.627).
+# Keyed by (kernel, pair strip rows): the instruction count per cell depends
+# on the strip height.
+VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 2.96,
+                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.63}
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
 # profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
