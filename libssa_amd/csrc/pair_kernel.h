@@ -410,7 +410,6 @@ pair_kernel(const StripArgs a) {
                     uint32_t F = perm(Fprev, rbv, SEL_LO_BHI_HI_ALO);
                     uint32_t hd = hd0;
                     uint32_t xs[2];
-                    uint32_t tt_prev = 0;        // NW: the previous row's h + Q
                     uint32_t flr = fl0;          // row r's floor (SW), advanced row by row
 #pragma unroll
                     for (int r = 0; r < NPS; r++) {
@@ -435,17 +434,10 @@ pair_kernel(const StripArgs a) {
                         }
                         H[r] = h;
                         if (NW) {
-                            // diagonal-relative: E and F need no extension add.
-                            // The previous row's E update sits between this
-                            // row's h and tt: a dependent use of a packed max
-                            // right after it costs an s_nop on gfx950, and NW's
-                            // chain h -> tt -> F -> h leaves nothing else to
-                            // put there (E[r] is next read at the next column)
-                            if (r > 0) E[r - 1] = fmax2(E[r - 1], tt_prev);
+                            // diagonal-relative: E and F need no extension add
                             const uint32_t tt = h + cQ;
+                            E[r] = fmax2(E[r], tt);
                             F = fmax2(F, tt);
-                            tt_prev = tt;
-                            if (r == NPS - 1) E[r] = fmax2(E[r], tt);
                         } else {
                             const uint32_t tt = h + cQ;
                             E[r] = fmax3(E[r], tt, flr);
