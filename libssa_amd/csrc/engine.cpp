@@ -1685,7 +1685,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         if (!lean) check(hipEventRecord(D.ev[4], st), "event");
         if (!qpt.empty())
             check(hipMemcpyAsync(dqpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
-        check(hipMemcpyAsync(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
+        if (C.upload_kernel)
+            check(launch_upload(dup, up_m, (blk_bytes + 3) & ~(size_t)3, st), "upload kernel");
+        else
+            check(hipMemcpyAsync(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
         if (piped) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
         // overflow list of this view: the whole list, or in a multi-view
         // search its own slice (all views stay on the device until the end)

@@ -406,5 +406,7 @@ struct TableArgs {
     uint32_t nzero_hdr;        // when the re-score tier runs beside the filter instead of before it)
 };
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st);
+// dst (device) <- src (pinned host), bytes a multiple of 4: a kernel on st
+hipError_t launch_upload(void* dst, const void* src, size_t bytes, hipStream_t st);
 
 }  // namespace ssa

@@ -863,6 +863,25 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
     }
 }
 
+// The per-search upload block read straight from pinned host memory by a
+// kernel on the search's own stream (option "upload_kernel"): no hand-off to
+// a copy engine and back before the tables kernel.  System-scope loads: the
+// staging buffer is rewritten by the host for every search, so no cache line
+// of an earlier search's read may serve this one.
+__global__ void __launch_bounds__(256) upload_kernel(uint32_t* dst, const uint32_t* src, uint32_t n4) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_upload(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return hipSuccess;
+    if ((bytes & 3) || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3)) return hipErrorInvalidValue;
+    const uint32_t n4 = (uint32_t)(bytes / 4);
+    const uint32_t blocks = std::min<uint32_t>((n4 + 255) / 256, 64);
+    hipLaunchKernelGGL(upload_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)dst, (const uint32_t*)src, n4);
+    return hipGetLastError();
+}
+
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const uint32_t prow = a.alpha + 1;
     const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);

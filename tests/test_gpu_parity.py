@@ -1361,6 +1361,33 @@ def test_search_batch_matches_single_queries():
             S.free_sequence(q)
 
 
+@pytest.mark.parametrize("upload", [1, 0])
+def test_upload_kernel_new_query_every_search(upload):
+    """Option upload_kernel: the per-search upload block (matrix, boundary,
+    query) read from the pinned staging buffer by a kernel with system-scope
+    loads.  The buffer is rewritten for every search, so consecutive searches
+    with different queries, matrices and gaps must each see their own block."""
+    codes, off = syn.protein_db(3000, 31, lo=1, hi=500)
+    ids = np.arange(len(off) - 1, dtype=np.uint64)
+    S.set_option("upload_kernel", upload)
+    try:
+        with tempfile.TemporaryDirectory() as tmp:
+            for rnd, (mname, go, ge) in enumerate([("blosum62", -11, -1), ("blosum50", -10, -2), ("blosum62", -3, -1)]):
+                configure(False, ("builtin", mname), go, ge)
+                if rnd == 0:
+                    S.init_db(_write_db(tmp, codes, off))
+                M = TABLES["matrices"][NAMES.index(mname)].copy()
+                for n in (40, 333, 100, 401):
+                    q = syn.protein_query(n, 500 + n + rnd)
+                    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+                    for algo, fn in ((S.SW, S.sw_align), (S.NW, S.nw_align)):
+                        exp = po.scores(algo, q, codes, off, M, go, ge)
+                        assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, ids, 10), (upload, mname, n, algo)
+                    S.free_sequence(qq)
+    finally:
+        S.set_option("upload_kernel", 0)
+
+
 def test_search_batch_pipelined_sub_batches():
     """Batches beyond one pipelined sub-batch (16 queries), every k up to the
     device filter's 64, a lone last query, and overflowing queries (int64
