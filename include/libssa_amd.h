@@ -118,8 +118,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
  *                        merges at the list width k needs, for DBs of <= 256 filter blocks
  *                        (default), or always the general scan
- *   "upload_kernel" 0|1  1: the per-search upload block (matrix, boundary, query) is read from pinned
- *                        host memory by a kernel on the search's stream, not a copy-engine transfer
+ *   "upload_kernel" 1|0  1 (default): the per-search upload block (matrix, boundary, query) is read
+ *                        from pinned host memory by a kernel on the search's stream; 0: a
+ *                        copy-engine transfer (hipMemcpyAsync)
  *   "tier_defer" 1|0     single-view searches: the exact re-score tier runs only when the device
  *                        filter's header reports overflowed lanes, after the result's copy
  *                        (default 1); 0: always, between the DP kernels and the filter

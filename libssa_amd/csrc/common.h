@@ -42,8 +42,9 @@ struct Config {
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
     int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
     int long16 = 1;                       // SW long entries on packed 16-bit patterns (long16_kernel) when exact
-    int upload_kernel = 0;                // 1: the per-search upload block is read from pinned memory by a kernel
-                                          // on the search's stream instead of a copy-engine transfer
+    int upload_kernel = 1;                // 1: the per-search upload block is read from pinned memory by a kernel
+                                          // on the search's stream instead of a copy-engine transfer (-14 us
+                                          // between searches, profiles/r05/host_gap/kgap_upk*.txt)
     int tier_defer = 1;                   // single-view searches: the int32 re-score tier runs after the result's
                                           // copy, only when the search has overflowed lanes
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry

@@ -1385,7 +1385,7 @@ def test_upload_kernel_new_query_every_search(upload):
                         assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, ids, 10), (upload, mname, n, algo)
                     S.free_sequence(qq)
     finally:
-        S.set_option("upload_kernel", 0)
+        S.set_option("upload_kernel", 1)
 
 
 def test_search_batch_pipelined_sub_batches():
