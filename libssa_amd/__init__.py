@@ -212,6 +212,14 @@ def align_scores(q, hitcount, bit_width=BIT_WIDTH_16, algo=SW):
     return out
 
 
+def align_free(q, hitcount, bit_width=BIT_WIDTH_16, algo=SW):
+    """free_alignment(sw_align(...)) / free_alignment(nw_align(...)) with the
+    hits unread: the call the reference's benchmark times
+    (benchmark/src/benchmark_util.c:27-48)."""
+    L = load()
+    L.free_alignment((L.sw_align if algo == SW else L.nw_align)(q, hitcount, bit_width, COMPUTE_SCORE))
+
+
 def nw_align(q, hitcount, bit_width=BIT_WIDTH_16, align_type=COMPUTE_SCORE):
     L = load()
     al = L.nw_align(q, hitcount, bit_width, align_type)

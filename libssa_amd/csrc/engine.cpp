@@ -2390,8 +2390,13 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                       "D2H exact scores");
             }
             if (!host_direct) {
-                // one copy: counters (incl. the overflow counts) + the first candidates
-                const size_t first = std::min<size_t>(D.h_cand_cap, f.n);
+                // one copy: counters (incl. the overflow counts) + the first
+                // candidates -- twice the last search's count, at least 256
+                // (a short copy is most of a copy's latency; more candidates
+                // than that come in a second copy after the synchronisation)
+                const size_t first = std::min<size_t>(std::min<size_t>(D.h_cand_cap, f.n),
+                                                      std::max<size_t>(256, 2 * (size_t)D.cand_hint + 64));
+                D.cand_first = first;
                 check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
                       "D2H candidates");
             }
@@ -2522,7 +2527,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             const uint32_t nc = D.h_fbuf[0];
             const uint2* cand = (const uint2*)(D.h_fbuf + kFilterHeader);
             std::vector<uint2> more;
-            if (nc > D.h_cand_cap) {
+            // (the filter wrote its result to pinned memory itself: up to h_cand_cap)
+            const size_t have = host_direct ? D.h_cand_cap : D.cand_first;
+            D.cand_hint = nc;
+            if (nc > have) {
                 more.resize(nc);
                 check(hipMemcpy(more.data(), D.d_fbuf + kFilterHeader, 8 * (size_t)nc, hipMemcpyDeviceToHost),
                       "D2H candidates");

@@ -45,6 +45,8 @@ struct DeviceDB {
     int32_t* d_thresh_local = nullptr;
     uint32_t* h_fbuf = nullptr;           // pinned: counters + h_cand_cap candidates
     size_t h_cand_cap = 0;
+    size_t cand_first = 0;                // candidates the last single-view search copied with its counters
+    uint32_t cand_hint = 0;               // the last single-view search's candidate count (sizes that copy)
     uint8_t* h_up = nullptr;              // pinned staging for per-search uploads
     size_t h_up_cap = 0;
     int32_t* d_scores = nullptr;
