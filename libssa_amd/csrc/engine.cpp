@@ -1810,6 +1810,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             tl = D.d_timeline;
         }
         check(hipEventRecord(ev_k0, st), "event");
+        std::vector<std::function<void()>> long_launch;   // the long-entry kernels' launches
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
         size_t lds_long = pair_lds;   // LDS of a long workgroup (the pair tables' gate)
@@ -1895,30 +1896,36 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             la.timeline = tl;
             if (use_pair) la.lds_min = (uint32_t)pair_lds;
             gate_base = gate_total;
+            // (issued right after the tables kernel below: the host issues
+            // the next GPU step first, and the tables kernel's gate holds the
+            // pair kernel until these workgroups have started)
             if (long4 > 0) {
                 la.seq0 = 0;
                 la.nseq = long4 * 64;
                 gate_total += la.nseq;                         // one workgroup per entry
                 D.gate_count += la.nseq;
-                check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
-                check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
-                check(hipEventRecord(D.ev[7], D.stream_long), "event");
+                long_launch.push_back([=, &D]() {
+                    check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
+                    check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
+                    check(hipEventRecord(D.ev[7], D.stream_long), "event");
+                });
             }
             if (long4 < long_groups) {
                 la.seq0 = long4 * 64;
                 la.nseq = (long_groups - long4) * 64;
                 gate_total += (la.nseq + kLongWaves - 1) / kLongWaves;   // four entries per workgroup
                 D.gate_count += (la.nseq + kLongWaves - 1) / kLongWaves;
-                check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
                     la.extra16 = extra16;
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
-                    check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
-                } else {
-                    check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
                 }
-                check(hipEventRecord(D.ev[6], D.stream_long1), "event");
+                long_launch.push_back([=, &D]() {
+                    check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
+                    if (rl16 > 0) check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
+                    else check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
+                    check(hipEventRecord(D.ev[6], D.stream_long1), "event");
+                });
             }
             if (v == 0) {
                 lentries = long_groups * 64;
@@ -1932,9 +1939,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                                                    : long4 > 0 ? long_lds_bytes(la.alpha, 4, rl4)
                                                                : long_lds_bytes(la.alpha, 1, rl1));
         }
-        // the pair tables after the long entries' launch: long_kernel only
-        // needs the uploads, so its workgroups are dispatched before the
-        // pair kernel's fill the CUs' LDS (they are the critical path)
+        // the pair tables, then the long entries' launches: the tables kernel
+        // runs while the host issues them, and its gate (block 0) holds the
+        // pair kernel until their workgroups have started -- they are the
+        // critical path and must be placed before the pair kernel's fill the
+        // CUs' LDS
         if (use_pair) {
             TableArgs ta{};
             ta.query = D.d_query;
@@ -1975,6 +1984,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         } else {
             check(hipMemsetAsync(ovf, 0, 4, st), "memset");
         }
+        for (auto& f : long_launch) f();
 
         if (use_pair) {
             StripArgs b = a;
