@@ -18,6 +18,9 @@
 
 namespace ssa {
 
+// (events: see upload_pack)
+static const unsigned kEventFlags = hipEventReleaseToDevice;
+
 ssa_amd_stats_t& stats() {
     static ssa_amd_stats_t s;
     return s;
@@ -408,7 +411,11 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         }
         check(hipStreamCreateWithPriority(&D.stream_long, hipStreamNonBlocking, prio_hi), "hipStreamCreate");
         check(hipStreamCreateWithPriority(&D.stream_long1, hipStreamNonBlocking, prio_hi), "hipStreamCreate");
-        for (auto& e : D.ev) check(hipEventCreate(&e), "hipEventCreate");
+        // every event of a search orders work on this device (timing
+        // markers, the long kernels' join, the staging buffer's reuse): a
+        // device-scope release, not a system-scope one (an L2 writeback of
+        // the search's row-buffer lines each time, ~5 us on the path)
+        for (auto& e : D.ev) check(hipEventCreateWithFlags(&e, kEventFlags), "hipEventCreate");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
             D.nsimd = (uint32_t)cus * 4;
@@ -1318,7 +1325,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         }
         while (D.vev.size() < 2 * V + 1) {
             hipEvent_t e;
-            check(hipEventCreate(&e), "hipEventCreate");
+            check(hipEventCreateWithFlags(&e, kEventFlags), "hipEventCreate");
             D.vev.push_back(e);
         }
     }
