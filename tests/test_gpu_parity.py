@@ -476,6 +476,19 @@ def test_long16_kernel_vs_oracle(qlen):
 
 
 
+@pytest.mark.parametrize("gate", [0, 1])
+def test_long_entries_without_the_gate(gate):
+    """Option long_gate 0: the pair kernel does not wait for the long-entry
+    workgroups to start (they are issued after the tables kernel, on the
+    highest-priority streams) -- the scheduling changes, the scores do not."""
+    S.set_option("long_gate", gate)
+    try:
+        _long_entry_case(400, S.SW, (-11, -1), 1, huge=True, long16=1)
+        _long_entry_case(513, S.NW, (-11, -1), 0, huge=True)
+    finally:
+        S.set_option("long_gate", 1)
+
+
 @pytest.mark.parametrize("qlen", [1025, 1032, 1500, 2056, 262, 513])
 @pytest.mark.parametrize("rows", [1, 0, 2])
 def test_long16_row_scan(qlen, rows):
