@@ -124,8 +124,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "tier_defer" 1|0     single-view searches: the exact re-score tier runs only when the device
  *                        filter's header reports overflowed lanes, after the result's copy
  *                        (default 1); 0: always, between the DP kernels and the filter
- *   "long_gate" 1|0      the pair kernel starts after the long-entry workgroups have (default 1;
- *                        0: no wait, the long-entry streams' priority alone orders them)
+ *   "long_gate" 1|0|P    the pair kernel starts after the long-entry workgroups have (default 1;
+ *                        0: no wait, the long-entry streams' priority alone orders them; 2..99:
+ *                        after the first P % of them)
  *   "long16_rows" 1|0|2  queries beyond 1 024 rows: long16 passes planned by issue cost, up to 8
  *                        last rows scored by a row scan (default 1); 0: RL 16 passes; 2: the
  *                        cost model at every query length (q = 513: RL 8 + 1 scanned row)

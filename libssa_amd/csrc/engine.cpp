@@ -1984,8 +1984,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 // first in order)
                 const uint32_t resident = (uint32_t)std::max<size_t>(1, pair_wgs_per_cu(lds_long)) *
                                           (D.nsimd / 4);
+                uint32_t want = std::min<uint32_t>(gate_total - gate_base, std::min<uint32_t>(512, resident));
+                // (option long_gate P > 1: only the first P % of them)
+                if (C.long_gate > 1 && C.long_gate < 100) want = std::max<uint32_t>(1, want * (uint32_t)C.long_gate / 100);
                 ta.gate = gate;
-                ta.gate_target = gate0 + std::min<uint32_t>(gate_total, gate_base + std::min<uint32_t>(512, resident));
+                ta.gate_target = gate0 + gate_base + want;
             }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {
