@@ -153,9 +153,9 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        the filter into pinned host memory (1: system-scope release, 2: system-
  *                        scope stores, the host spinning on a sequence word; 3: plain stores,
  *                        published by the end of the dispatch, the host synchronising as usual)
- *   "sync_spin" 0|1      1: the host spins while a search runs (hipDeviceScheduleSpin, set at the
- *                        library's first pack on a device); 0 (default): HIP's own scheduling
- *                        (no difference measured, profiles/r05/ab/sync_spin)
+ *   "sync_spin" 1|0      1 (default): the host thread spins while a search runs (hipDeviceScheduleSpin,
+ *                        set at the library's first pack on a device; 15 us less between two
+ *                        searches); 0: HIP's own scheduling (yields the core)
  *   "lean_events" 1|0    1 (default): no timing markers around the upload, the re-score tier
  *                        and the filter (stats upload_ms, wide_ms, d2h_ms read 0; kernel_ms
  *                        kept; C2 +0.5 %, profiles/r05/ab/lean_events); 0: all markers

@@ -61,9 +61,9 @@ struct Config {
     int counters = -1;                    // the reference's 8/16-bit overflow counters: -1 auto (output mode
                                           // >= INFO, when m_run prints them), 0 never, 1 always
     int pair_prio_groups = 0;             // pair_kernel groups at raised wave priority: -1 one per SIMD, 0 none (measured neutral)
-    int sync_spin = 0;                    // 1: hipDeviceScheduleSpin for this library's devices (set at the first
+    int sync_spin = 1;                    // 1: hipDeviceScheduleSpin for this library's devices (set at the first
                                           // pack on a device): the host spins, not yields, while a search runs
-                                          // (default 0: no difference measured, profiles/r05/ab/sync_spin)
+                                          // (-15 us between searches, profiles/r05/host_gap/kgap_spin.txt)
     int lean_events = 1;                  // 1 (default): no timing markers around the upload, the tier and the filter
                                           // (stats upload_ms / wide_ms / d2h_ms stay 0; kernel_ms kept;
                                           // C2 +0.5 %, profiles/r05/ab/lean_events)

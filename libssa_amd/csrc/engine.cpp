@@ -395,10 +395,11 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     if (!D.stream) {
         // how the host waits for a search (option "sync_spin"): HIP's default
         // on a machine with more CPUs than contexts yields the waiting thread;
-        // spinning keeps it on its core (no end-to-end difference measured,
-        // profiles/r05/ab/sync_spin, so off by default).  Set before this
-        // library's first use of the device; a context another runtime user
-        // made first keeps its flags (the call's error is cleared)
+        // spinning keeps it on its core -- 15 us less from the result's copy
+        // to the next search's first launch (profiles/r05/host_gap/kgap_spin.txt
+        // vs kgap_nospin.txt, one box).  Set before this library's first use
+        // of the device; a context another runtime user made first keeps its
+        // flags (the call's error is cleared)
         if (C.sync_spin && hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
         // the long-entry kernels' streams at the device's highest priority:
