@@ -47,6 +47,7 @@ struct Config {
                                           // between searches, profiles/r05/host_gap/kgap_upk*.txt)
     int tier_defer = 1;                   // single-view searches: the int32 re-score tier runs after the result's
                                           // copy, only when the search has overflowed lanes
+    int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry
                                           // workgroups have started (TableArgs::gate)
     int long16_rows = 1;                  // long16_kernel may leave up to 8 query rows to its row scan (LongArgs::extra16)

@@ -40,6 +40,11 @@ __device__ __forceinline__ void load_row(uint32_t (&dst)[NP], const uint32_t* ro
         dst[4 * i + 2] = v.z;
         dst[4 * i + 3] = v.w;
     }
+    if constexpr (NP % 4 == 2) {
+        const uint2 v = *(const uint2*)(row + NP - 2);
+        dst[NP - 2] = v.x;
+        dst[NP - 1] = v.y;
+    }
 }
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));

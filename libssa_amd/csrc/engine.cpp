@@ -1926,6 +1926,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 if (rl16 > 0) {
                     la.base16 = long16_base(Q, R);
                     la.extra16 = extra16;
+                    la.low_prio = C.long_prio ? 0u : 1u;
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
                 }
                 long_launch.push_back([=, &D]() {

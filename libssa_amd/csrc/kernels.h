@@ -30,6 +30,12 @@ constexpr size_t pair_wgs_per_cu(size_t bytes) {
 }
 constexpr int kF16Floor = 0x0800;  // pattern of the SW zero in strip_f16m_kernel
 
+// pair_kernel tail strips of 2*npt rows: npt a multiple of 4, or of 2 for the
+// default strip heights (SW 48 rows, NW 64/80) after at least one main strip
+// -- the tail's table then has a padded global pitch of round4(npt) dwords
+__host__ __device__ constexpr bool pair_tail_fine(int np, bool nw) { return nw ? (np == 32 || np == 40) : np == 24; }
+__host__ __device__ constexpr uint32_t pair_tail_pitch(uint32_t npt) { return (npt + 3) & ~3u; }
+
 constexpr int kMaxFuse = 16;       // queries one pair_kernel launch may score (StripArgs::nq)
 
 struct GroupDesc {
@@ -156,6 +162,7 @@ struct LongArgs {
     // one row at a time after its passes (a prefix maximum over 64 columns
     // per step, kernels.hip long16_rows), from the last pass's bottom row
     uint32_t extra16;
+    uint32_t low_prio;         // long16_kernel: 1 = no raised wave priority (option "long_prio" 0)
     // long_kernel (W = 1) as the exact int32 re-score tier of the DP kernels'
     // overflowed lanes (engine.cpp): when `list` is set the entries are the
     // lanes list[0 .. min(*list_count, nseq)), in a grid of `blocks`

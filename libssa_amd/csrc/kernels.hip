@@ -1591,7 +1591,9 @@ __global__ void __launch_bounds__(64 * kLongWaves) long16_kernel(const LongArgs 
     constexpr uint32_t CS = 64 * SLW;                // dwords per code
     constexpr uint32_t RP = 64 * RL;                 // rows per pass
     constexpr int PF = 2;                            // profile loads issued PF steps ahead
-    __builtin_amdgcn_s_setprio(3);
+    // (raised issue priority over the pair waves sharing the SIMD, unless
+    // LongArgs::low_prio: option "long_prio" 0)
+    if (!a.low_prio) __builtin_amdgcn_s_setprio(3);
     const uint32_t t_start = a.timeline ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     if (a.gate && threadIdx.x == 0)
         __hip_atomic_fetch_add(a.gate, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);

@@ -53,7 +53,7 @@ namespace ssa {
 // inside the last block.
 // ---------------------------------------------------------------------------
 // row groups of the SW anti-diagonal maxima: 16, then 8, then 4 rows
-constexpr int ad_size_at(int s, int np) { return np - s >= 16 ? 16 : (np - s >= 8 ? 8 : 4); }
+constexpr int ad_size_at(int s, int np) { return np - s >= 16 ? 16 : (np - s >= 8 ? 8 : (np - s >= 4 ? 4 : 2)); }
 constexpr int ad_start(int r, int np) {
     int s = 0;
     while (r >= s + ad_size_at(s, np)) s += ad_size_at(s, np);
@@ -77,6 +77,8 @@ constexpr int pair_occupancy(int np, bool) { return np <= 16 ? 4 : (np <= 24 ? 3
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const u32x4 lds_u4;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const u32x2 lds_u2;
 
 // Strip parts (StripArgs::nparts = 2 or 3) hand a group's boundary rows from
 // the workgroup of part p-1 (XCD A) to that of part p (maybe XCD B; the XCDs'
@@ -251,13 +253,16 @@ pair_kernel(const StripArgs a) {
         // global table's (A+1)^2 rows (row c1 * prow + c0)
         __syncthreads();
         const uint32_t A_ = a.alpha;
-        const uint32_t ntab4 = pair_lds_rows(A_) * (NPS / 4);
+        // (table rows of NPS dwords at a pitch of whole 16-byte units: a tail
+        // of NPS = 2 mod 4 rows has a padded global pitch, pair_tables_kernel)
+        constexpr uint32_t NP4 = (NPS + 3) / 4;
+        const uint32_t ntab4 = pair_lds_rows(A_) * NP4;
         const uint4* src = (const uint4*)tab;
         for (uint32_t i = threadIdx.x; i < ntab4; i += 64 * W) {
-            const uint32_t lrow = i / (NPS / 4), k = i % (NPS / 4);
+            const uint32_t lrow = i / NP4, k = i % NP4;
             const uint32_t c1 = lrow < (A_ + 1) * A_ ? lrow / A_ : A_;
             const uint32_t c0 = lrow < (A_ + 1) * A_ ? lrow - c1 * A_ : A_;
-            *(uint4*)(lds + lrow * ROWW + 4 * k) = src[(c1 * prow + c0) * (NPS / 4) + k];
+            *(uint4*)(lds + lrow * ROWW + 4 * k) = src[(c1 * prow + c0) * NP4 + k];
         }
         __syncthreads();
         if (!active) return;
@@ -424,6 +429,11 @@ pair_kernel(const StripArgs a) {
                             P[r - 2] = v.y;
                             P[r - 1] = v.z;
                             P[r] = v.w;
+                        } else if (NPS % 4 == 2 && r == NPS - 1) {
+                            // (a tail of NPS = 2 mod 4 rows: its last two)
+                            const u32x2 v = *(const lds_u2*)(nrow + r - 1);
+                            P[r - 1] = v.x;
+                            P[r] = v.y;
                         }
                         hd = H[r];
                         const int g0 = ad_start(r, NPS), G = ad_size(r, NPS);
@@ -595,14 +605,17 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     return hipGetLastError();
 }
 
-template <int NP, bool NW, int NPT = 4>
+template <int NP, bool NW, int NPT = 2>
 static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st, int* occ) {
-    // npt in {0} + multiples of 4 up to NP
-    if constexpr (NPT == 4) {
+    // npt in {0} + multiples of 4 up to NP, and for the default strip heights
+    // (pair_tail_fine) the multiples of 2
+    constexpr int STEP = pair_tail_fine(NP, NW) ? 2 : 4;
+    if constexpr (NPT == 2) {
         if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st, occ);
+        if constexpr (STEP == 4) return launch_pair_np<NP, NW, 4>(a, npt, lds_bytes, st, occ);
     }
     if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st, occ);
-    if constexpr (NPT + 4 <= NP) return launch_pair_np<NP, NW, NPT + 4>(a, npt, lds_bytes, st, occ);
+    if constexpr (NPT + STEP <= NP) return launch_pair_np<NP, NW, NPT + STEP>(a, npt, lds_bytes, st, occ);
     return hipErrorInvalidValue;
 }
 
