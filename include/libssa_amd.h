@@ -124,6 +124,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "tier_defer" 1|0     single-view searches: the exact re-score tier runs only when the device
  *                        filter's header reports overflowed lanes, after the result's copy
  *                        (default 1); 0: always, between the DP kernels and the filter
+ *   "tail_rows4" 1|0     the pair kernel's last strip at 4-row granularity (default; SW 48-row and
+ *                        NW 64/80-row strips, after a main strip), or 8-row (0)
  *   "long_prio" 1|0      long16 waves at raised issue priority over the pair waves (default 1)
  *   "long_gate" 1|0|P    the pair kernel starts after the long-entry workgroups have (default 1;
  *                        0: no wait, the long-entry streams' priority alone orders them; 2..99:

@@ -452,6 +452,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "long16_rows")) cfg().long16_rows = (int)value;
     else if (!strcmp(name, "long_gate")) cfg().long_gate = (int)value;
     else if (!strcmp(name, "long_prio")) cfg().long_prio = (int)value;
+    else if (!strcmp(name, "tail_rows4")) cfg().tail_rows4 = (int)value;
     else if (!strcmp(name, "tier_defer")) cfg().tier_defer = (int)value;
     else if (!strcmp(name, "upload_kernel")) cfg().upload_kernel = (int)value;
     else if (!strcmp(name, "filter_prefix_regs")) set_filter_prefix_regs((int)value);

@@ -47,6 +47,7 @@ struct Config {
                                           // between searches, profiles/r05/host_gap/kgap_upk*.txt)
     int tier_defer = 1;                   // single-view searches: the int32 re-score tier runs after the result's
                                           // copy, only when the search has overflowed lanes
+    int tail_rows4 = 1;                   // pair kernel tail strips at 4-row granularity (default heights)
     int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry
                                           // workgroups have started (TableArgs::gate)

@@ -1167,13 +1167,16 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
         const uint32_t rem = (uint32_t)(m % Hm);
         if (rem > 0) {
             tail_np = (int)(rem + 7) / 8 * 4;     // 8-row granularity
+            // 4-row granularity after a main strip, for the default heights
+            // (q = 513: a 36-row tail instead of 40 for the last 33 rows)
+            if (C.tail_rows4 && full > 0 && pair_tail_fine(pnp, nw)) tail_np = (int)(rem + 3) / 4 * 2;
         } else if (nw) {
             full--;
             tail_np = pnp;
         }
         main_strips = full;
         tail_off = (size_t)full * prow * prow * pnp;
-        qpt_words = tail_off + (size_t)prow * prow * tail_np;
+        qpt_words = tail_off + (size_t)prow * prow * pair_tail_pitch((uint32_t)tail_np);
     }
     vp.A = A;
     vp.prow = prow;

@@ -842,19 +842,22 @@ __global__ void __launch_bounds__(256) pair_tables_kernel(const TableArgs a) {
     const uint32_t prow = a.alpha + 1;
     const uint32_t per_main = prow * prow * a.np;
     const uint32_t nmain = a.nmain * per_main;
-    const uint32_t total = nmain + prow * prow * a.npt;
+    // (the tail's rows at a pitch of whole 16-byte units: kernels.h pair_tail_pitch)
+    const uint32_t tpitch = pair_tail_pitch(a.npt);
+    const uint32_t total = nmain + prow * prow * tpitch;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        uint32_t ph, i0, rem;
+        uint32_t ph, pitch, i0, rem;
         if (t < nmain) {
-            ph = a.np;
+            ph = pitch = a.np;
             i0 = (t / per_main) * 2 * a.np;
             rem = t % per_main;
         } else {
             ph = a.npt;
+            pitch = tpitch;
             i0 = a.tail_row0;
             rem = t - nmain;
         }
-        const uint32_t pair = rem / ph, r = rem % ph;
+        const uint32_t pair = rem / pitch, r = rem % pitch;
         const uint32_t c1 = pair / prow, c0 = pair % prow;
         // "combined" signed constant lo + 65536 hi: one v_add_u32 adds it to a
         // packed pair of patterns exactly as two 16-bit adds would, since the
@@ -884,7 +887,7 @@ hipError_t launch_upload(void* dst, const void* src, size_t bytes, hipStream_t s
 
 hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const uint32_t prow = a.alpha + 1;
-    const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + a.npt);
+    const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + pair_tail_pitch(a.npt));
     if (total == 0) {
         if (a.zero_hdr) {
             const hipError_t e = hipMemsetAsync(a.zero_hdr, 0, 4 * a.nzero_hdr, st);

@@ -521,6 +521,46 @@ def test_long_entry_kernel_split_launches(qlen, algo):
     _long_entry_case(qlen, algo, (-11, -1), 0, huge=True, share4=50000)
 
 
+@pytest.mark.parametrize("algo,pnp,qlens", [
+    (S.SW, 24, (49, 50, 53, 54, 57, 61, 66, 70, 74, 78, 82, 86, 90, 94, 95, 97, 101, 141, 513)),
+    (S.NW, 40, (81, 82, 85, 89, 93, 97, 101, 105, 117, 121, 125, 133, 153, 157, 161, 165, 513)),
+    (S.NW, 32, (65, 66, 69, 73, 77, 90, 94, 126))])
+def test_tail_strip_four_row_granularity(algo, pnp, qlens):
+    """Option tail_rows4 (default): after at least one main strip, the pair
+    kernel's last strip is 4*k rows, not 8*k -- tails of 2 mod 4 packed rows
+    (a two-dword LDS reload for their last rows, a padded global table pitch,
+    2-row anti-diagonal groups).  Every remainder class against the oracle,
+    with the option on and off."""
+    rng = np.random.default_rng(pnp)
+    lens = np.array([0, 1, 2, 15, 16, 17, 47, 48, 49, 513] + list(rng.integers(1, 300, 200)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    keep = np.nonzero(lens > 0)[0]
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    fn = S.sw_align if algo == S.SW else S.nw_align
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        S.set_option("pair_np", pnp)
+        try:
+            for qlen in qlens:
+                q = syn.protein_query(qlen, 300 + qlen)
+                exp = po.scores(algo, q, codes, off, M, -11, -1)[keep]
+                qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+                for t4 in (1, 0):
+                    S.set_option("tail_rows4", t4)
+                    sc, ids = _full_scores(qq, algo, len(keep))
+                    assert (ids == keep).all()
+                    assert (sc == exp).all(), (qlen, t4, np.nonzero(sc != exp)[0][:10])
+                    assert S.stats()["kernel"].startswith("pair")
+                    assert [(h["score"], h["id"]) for h in fn(qq, 10, 16)] == po.topk(exp, keep.astype(np.uint64), 10)
+                S.free_sequence(qq)
+        finally:
+            S.set_option("pair_np", 0)
+            S.set_option("tail_rows4", 1)
+
+
 @pytest.mark.parametrize("gaps", [(0, 0), (-1, -4), (-5, -5), (-20, -7)])
 @pytest.mark.parametrize("qlen", [64, 513])
 @pytest.mark.parametrize("algo", [S.SW, S.NW])
