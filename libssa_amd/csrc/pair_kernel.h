@@ -609,14 +609,19 @@ template <int NP, bool NW, int NPT = 2>
 static hipError_t launch_pair_np(const StripArgs& a, int npt, size_t lds_bytes, hipStream_t st, int* occ) {
     // npt in {0} + multiples of 4 up to NP, and for the default strip heights
     // (pair_tail_fine) the multiples of 2
+    // (discarded branches, not early returns: a kernel named only behind a
+    // return is still instantiated by the device pass)
     constexpr int STEP = pair_tail_fine(NP, NW) ? 2 : 4;
-    if constexpr (NPT == 2) {
+    if constexpr (NPT == 2 && STEP == 4) {
         if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st, occ);
-        if constexpr (STEP == 4) return launch_pair_np<NP, NW, 4>(a, npt, lds_bytes, st, occ);
+        return launch_pair_np<NP, NW, 4>(a, npt, lds_bytes, st, occ);
+    } else {
+        if constexpr (NPT == 2)
+            if (npt == 0) return launch_pair_t<NP, NW, 0>(a, lds_bytes, st, occ);
+        if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st, occ);
+        if constexpr (NPT + STEP <= NP) return launch_pair_np<NP, NW, NPT + STEP>(a, npt, lds_bytes, st, occ);
+        else return hipErrorInvalidValue;
     }
-    if (npt == NPT) return launch_pair_t<NP, NW, NPT>(a, lds_bytes, st, occ);
-    if constexpr (NPT + STEP <= NP) return launch_pair_np<NP, NW, NPT + STEP>(a, npt, lds_bytes, st, occ);
-    return hipErrorInvalidValue;
 }
 
 }  // namespace ssa
