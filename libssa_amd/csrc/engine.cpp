@@ -967,7 +967,7 @@ struct PlanForce {
 };
 
 static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, const PlanForce* force, ViewPlan& vp,
-                      bool allow_merge = false) {
+                      bool allow_merge = false, bool batch = false) {
     const Config& C = cfg();
     const int Q = C.gap_open, R = C.gap_extend;
     const int64_t* M = matrix().m;
@@ -1168,8 +1168,10 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
         if (rem > 0) {
             tail_np = (int)(rem + 7) / 8 * 4;     // 8-row granularity
             // 4-row granularity after a main strip, for the default heights
-            // (q = 513: a 36-row tail instead of 40 for the last 33 rows)
-            if (C.tail_rows4 && full > 0 && pair_tail_fine(pnp, nw)) tail_np = (int)(rem + 3) / 4 * 2;
+            // (q = 513: a 36-row tail instead of 40 for the last 33 rows); a
+            // fused batch keeps 8-row tails (its queries share one plan, and
+            // finer tails would split batches of nearby lengths)
+            if (C.tail_rows4 && !batch && full > 0 && pair_tail_fine(pnp, nw)) tail_np = (int)(rem + 3) / 4 * 2;
         } else if (nw) {
             full--;
             tail_np = pnp;
@@ -1399,7 +1401,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         int64_t lo = INT64_MAX, hi = INT64_MIN;
         size_t mmax = 0;
         for (size_t v = 0; v < V && fused; v++) {
-            plan_view(D, views[v], nw, np, nullptr, fplans[v]);
+            plan_view(D, views[v], nw, np, nullptr, fplans[v], false, true);
             const ViewPlan &p = fplans[v], &p0 = fplans[0];
             fused = p.use_pair && !p.use_cls && p.pnp == p0.pnp && p.main_strips == p0.main_strips &&
                     p.tail_np == p0.tail_np;
@@ -1410,7 +1412,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         if (fused) {
             const PlanForce f{lo, hi, mmax, (uint32_t)V};
             for (size_t v = 0; v < V && fused; v++) {
-                plan_view(D, views[v], nw, np, &f, fplans[v]);
+                plan_view(D, views[v], nw, np, &f, fplans[v], false, true);
                 const ViewPlan &p = fplans[v], &p0 = fplans[0];
                 fused = p.use_pair && !p.use_cls && p.pnp == p0.pnp && p.main_strips == p0.main_strips &&
                         p.tail_np == p0.tail_np && p.long_groups == p0.long_groups && p.nmax16 == p0.nmax16 &&
