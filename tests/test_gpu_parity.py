@@ -1073,22 +1073,26 @@ def test_device_topk_filter_matches_full_scan(pattern):
 
 
 def _filter_candidates(sc, k):
-    """numpy restatement of the device filter's bound (kernels.hip, above
+    """numpy restatement of the device filter's bound (kernels.hip,
     filter_block): entry e of mini m (64 entries) of block b (4096) is
-    forwarded iff its score beats both the k-th largest maximum of the
-    earlier minis of b and the k-th largest maximum of all minis of the
-    blocks before b (INT32_MIN while fewer than k)."""
+    forwarded iff its score beats both the k-th largest value of the earlier
+    minis of b and the k-th largest value of all minis of the blocks before b
+    (INT32_MIN while fewer than k), where a mini's value is its maximum --
+    except the DB's first mini, which gives its k largest entries."""
     lo = np.iinfo(np.int32).min
     n = len(sc)
     nm, nb = -(-n // 64), -(-n // 4096)
     pad = np.full(nb * 4096, lo, np.int64)
     pad[:n] = sc
     mm = pad.reshape(nb * 64, 64).max(1).reshape(nb, 64)
+    vals = [[np.sort(pad[:64])[::-1][:k]] + [mm[0, m:m + 1] for m in range(1, 64)]]
+    vals += [[mm[b, m:m + 1] for m in range(64)] for b in range(1, nb)]
 
     def kth(v):
+        v = np.concatenate(v) if len(v) else np.zeros(0, np.int64)
         return lo if len(v) < k else int(np.sort(v)[::-1][k - 1])
-    t_block = np.array([kth(mm[:b].ravel()) for b in range(nb)], np.int64)
-    t_local = np.array([[kth(mm[b, :m]) for m in range(64)] for b in range(nb)], np.int64).ravel()[:nm]
+    t_block = np.array([kth([x for bb in vals[:b] for x in bb]) for b in range(nb)], np.int64)
+    t_local = np.array([[kth(vals[b][:m]) for m in range(64)] for b in range(nb)], np.int64).ravel()[:nm]
     e = np.arange(n)
     return int(np.count_nonzero(sc > np.maximum(t_block[e // 4096], t_local[e // 64])))
 
