@@ -29,6 +29,14 @@
 __global__ void k_small(unsigned* p, unsigned v) {
     if (blockIdx.x == 0 && threadIdx.x == 0) p[0] += v;
 }
+// (mode "spin": the long-entry and DP kernels hold one workgroup for a fixed
+// time, so the iteration shows whether the long branch overlaps the DP kernel)
+__global__ void k_spin(unsigned* p, unsigned ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+    if (threadIdx.x == 0) p[0] += 1;
+}
+static unsigned g_long_ticks = 0, g_pair_ticks = 0;   // 100 MHz ticks; 0: k_small
 
 struct Ctx {
     hipStream_t s, s2;
@@ -42,9 +50,11 @@ static void issue(Ctx& c, unsigned v) {
     CK(hipEventRecord(c.ek0, c.s));                                          // kernel_ms start
     hipLaunchKernelGGL(k_small, dim3(64), dim3(256), 0, c.s, c.d + 1, v);      // tables (gate target)
     CK(hipStreamWaitEvent(c.s2, c.ek0, 0));                                   // long stream fork
-    hipLaunchKernelGGL(k_small, dim3(64), dim3(256), 0, c.s2, c.d + 2, 1u);    // long kernel
+    if (g_long_ticks) hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, c.s2, c.d + 2, g_long_ticks);
+    else hipLaunchKernelGGL(k_small, dim3(64), dim3(256), 0, c.s2, c.d + 2, 1u);    // long kernel
     CK(hipEventRecord(c.e0, c.s2));
-    hipLaunchKernelGGL(k_small, dim3(1024), dim3(256), 0, c.s, c.d + 3, 1u);   // pair kernel
+    if (g_pair_ticks) hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, c.s, c.d + 3, g_pair_ticks);
+    else hipLaunchKernelGGL(k_small, dim3(1024), dim3(256), 0, c.s, c.d + 3, 1u);   // pair kernel
     CK(hipStreamWaitEvent(c.s, c.e0, 0));                                     // join
     CK(hipEventRecord(c.ek1, c.s));                                          // kernel_ms end
     hipLaunchKernelGGL(k_small, dim3(256), dim3(256), 0, c.s, c.d + 4, 1u);    // filter_block
@@ -58,7 +68,12 @@ static double med(std::vector<double> v) {
     return v[v.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
+    (void)argv;
+    if (argc > 1) {   // spin: long 200 us, DP 300 us
+        g_long_ticks = 20000;
+        g_pair_ticks = 30000;
+    }
     CK(hipSetDeviceFlags(hipDeviceScheduleSpin));
     Ctx c;
     int lo, hi;
@@ -72,7 +87,7 @@ int main() {
     CK(hipMalloc((void**)&c.d, 4096));
     CK(hipMemset(c.d, 0, 4096));
     CK(hipHostMalloc(&c.h, 4096, hipHostMallocDefault));
-    const int N = 2000;
+    const int N = argc > 1 ? 300 : 2000;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
 
@@ -141,8 +156,8 @@ int main() {
             }
         }
     }
-    printf("{\"iterations\": %d, \"direct_us\": %.1f, \"direct_issue_us\": %.1f, \"graph_us\": %.1f, "
+    printf("{\"mode\": \"%s\", \"iterations\": %d, \"direct_us\": %.1f, \"direct_issue_us\": %.1f, \"graph_us\": %.1f, "
            "\"graph_issue_us\": %.1f, \"graph_update_us\": %.1f, \"graph_update_issue_us\": %.1f}\n",
-           N, med(td), med(tsub), med(tg), med(tgs), tu.empty() ? -1.0 : med(tu), tus.empty() ? -1.0 : med(tus));
+           argc > 1 ? "spin: long 200 us, DP 300 us" : "trivial kernels", N, med(td), med(tsub), med(tg), med(tgs), tu.empty() ? -1.0 : med(tu), tus.empty() ? -1.0 : med(tus));
     return 0;
 }
