@@ -123,6 +123,11 @@ int main(int argc, char** argv) {
             tgs.push_back(us(t0, t1));
         }
     }
+    // the kernel_ms markers recorded by the graph's event nodes: readable?
+    float graph_kms = -1.0f;
+    const hipError_t ee = hipEventElapsedTime(&graph_kms, c.ek0, c.ek1);
+    if (ee != hipSuccess) graph_kms = -1.0f;
+    (void)hipGetLastError();
     // graph + one node's arguments per iteration (the tables kernel: second kernel node)
     size_t nn = 0;
     CK(hipGraphGetNodes(g, nullptr, &nn));
@@ -156,8 +161,32 @@ int main(int argc, char** argv) {
             }
         }
     }
-    printf("{\"mode\": \"%s\", \"iterations\": %d, \"direct_us\": %.1f, \"direct_issue_us\": %.1f, \"graph_us\": %.1f, "
-           "\"graph_issue_us\": %.1f, \"graph_update_us\": %.1f, \"graph_update_issue_us\": %.1f}\n",
-           argc > 1 ? "spin: long 200 us, DP 300 us" : "trivial kernels", N, med(td), med(tsub), med(tg), med(tgs), tu.empty() ? -1.0 : med(tu), tus.empty() ? -1.0 : med(tus));
+    // re-captured every iteration and swapped into the instantiated graph
+    // (hipGraphExecUpdate: same topology, new arguments), then launched
+    std::vector<double> tr, trs;
+    for (int i = 0; i < N + 50; i++) {
+        auto t0 = now();
+        hipGraph_t g2;
+        CK(hipStreamBeginCapture(c.s, hipStreamCaptureModeGlobal));
+        issue(c, (unsigned)i);
+        CK(hipStreamEndCapture(c.s, &g2));
+        hipGraphExecUpdateResult ur;
+        hipGraphNode_t en = nullptr;
+        CK(hipGraphExecUpdate(ge, g2, &en, &ur));
+        CK(hipGraphLaunch(ge, c.s));
+        auto t1 = now();
+        CK(hipStreamSynchronize(c.s));
+        auto t2 = now();
+        CK(hipGraphDestroy(g2));
+        if (i >= 50) {
+            tr.push_back(us(t0, t2));
+            trs.push_back(us(t0, t1));
+        }
+    }
+    printf("{\"recapture_us\": %.1f, \"recapture_issue_us\": %.1f, ", med(tr), med(trs));
+    printf("\"mode\": \"%s\", \"iterations\": %d, \"direct_us\": %.1f, \"direct_issue_us\": %.1f, \"graph_us\": %.1f, "
+           "\"graph_issue_us\": %.1f, \"graph_update_us\": %.1f, \"graph_update_issue_us\": %.1f, \"graph_event_elapsed_us\": %.1f, \"graph_event_status\": \"%s\"}\n",
+           argc > 1 ? "spin: long 200 us, DP 300 us" : "trivial kernels", N, med(td), med(tsub), med(tg), med(tgs), tu.empty() ? -1.0 : med(tu), tus.empty() ? -1.0 : med(tus),
+           graph_kms * 1000.0, hipGetErrorName(ee));
     return 0;
 }
