@@ -32,6 +32,18 @@ def test_libraries_built():
     S.load()
 
 
+@pytest.mark.parametrize("obj", ["kernels", "pair_sw", "pair_nw", "counters"])
+def test_hip_objects_hold_every_registered_kernel(obj):
+    """Every kernel the host half of a HIP object registers is in its gfx950
+    code object (tools/check_kernels.sh, also run by the Makefile): a launch
+    of a host-only stub aborts the process on the GPU."""
+    path = os.path.join(ROOT, "libssa_amd", "build", obj + ".o")
+    if not os.path.exists(path):
+        pytest.skip("no in-tree build objects")
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "check_kernels.sh"), path], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
 @pytest.mark.parametrize("header,lib", [("libssa.h", "libssa_amd.so"), ("libssa_amd.h", "libssa_amd.so"),
                                         ("libssa_extern_db.h", "libssa_fasta_db.so")])
 def test_every_declared_symbol_is_exported(header, lib):
