@@ -111,6 +111,11 @@ def parse():
                    help="skip the north_star record (SW int16, q = 400 vs the fixed 10 M-sequence DB, strong)")
     p.add_argument("--north-star-steps", type=int, default=None, help="timed steps of the north_star record "
                    "(default: --steps, at most 10)")
+    p.add_argument("--no-drop-in", action="store_true",
+                   help="N>1: skip the drop_in record (the north-star DB through sw_align on all N devices of "
+                        "rank 0's process, after the multi-process records)")
+    p.add_argument("--drop-in-seqs", type=int, default=None,
+                   help="drop_in record: the first S IDs of the north-star DB instead of all 10 M")
     p.add_argument("--long-tail", type=int, default=None,
                    help="replace N DB sequences by 5k-35k-residue ones (a UniProt-like length tail)")
     p.add_argument("--strip-np", type=int, default=16, help="int16/f16m strip kernels: packed rows per strip")
@@ -381,6 +386,7 @@ class Job:
 
     def __init__(self, rank, world, dist, dev, backend):
         self.rank, self.world, self.dist, self.dev, self.backend = rank, world, dist, dev, backend
+        self.dev_index = 0           # this rank's GPU (ssa_amd_set_device)
         self.native = False          # ssa_amd_gather_logs over RCCL
         self.gather_note = None
         self.rccl_ranks = None
@@ -723,6 +729,95 @@ def north_star(S, args, job):
     return rec
 
 
+def drop_in(S, args, job, torch_sync=None):
+    """N > 1, after the multi-process records: the drop-in path -- an
+    UNCHANGED libssa caller on all N GPUs of the node from ONE process, as
+    SSA_AMD_DEVICES routes it (include/libssa_amd.h: the library's persistent
+    per-device slot threads inside sw_align, the DB split into chunk-aligned
+    residue-balanced record ranges, the slot logs merged on the host; the
+    reference's own default is every core of the machine,
+    src/util/thread_pool.c:39-47, its heaps merged in thread order,
+    src/algo/manager.c:141-145).  Ranks != 0 release their device DBs
+    (ssa_exit) and wait at a barrier; rank 0 opens the north-star DB (the
+    fixed 10 M sequences; --drop-in-seqs: its first S IDs), selects one device
+    slot per rank (ssa_amd_set_devices -- a rehearsal's ranks share GPUs, so
+    do its slots) and times free_alignment(sw_align(...)) exactly as the N = 1
+    headline.  Returns rank 0's record (None elsewhere)."""
+    if job.rank != 0:
+        S.ssa_exit()
+        job.dist.barrier()
+        return None
+    S.ssa_exit()
+    w = workload(args, "north_star", overrides=False)
+    n_gpus = max(1, args.n_gpus)
+    devices = [r % n_gpus for r in range(job.world)]
+    from libssa_amd import synthetic as syn
+    t0 = time.time()
+    configure(S, w)
+    q = W.query(w.cfg, w.qlen)
+    _, total, job_ids = W.cuts(w.cfg, 1, q, args.drop_in_seqs, w.lengths)
+    codes, off = W.slice_db(w.cfg, q, total, 0, job_ids, w.alphabet, w.lengths)
+    tmpdir = tempfile.mkdtemp(prefix="ssa_dropin_")
+    path = os.path.join(tmpdir, "db.fas")
+    syn.write_fasta(path, codes, off)
+    residues, seqs = int(off[-1]), len(off) - 1
+    del codes, off
+    assert S.set_devices(devices) == 0, devices
+    S.init_db(path)
+    S.set_id_offset(0)
+    S.prepare_db()
+    os.remove(path)
+    os.rmdir(tmpdir)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    setup_s = time.time() - t0
+    steps = args.north_star_steps if args.north_star_steps is not None else min(args.steps, 10)
+    k = args.k
+    S.align_free(qq, k, w.width, S.SW)                      # warm-up
+    st0 = S.stats()
+    if torch_sync:
+        torch_sync()
+    ts = time.perf_counter()
+    for _ in range(steps):
+        S.align_free(qq, k, w.width, S.SW)
+    if torch_sync:
+        torch_sync()
+    elapsed = time.perf_counter() - ts
+    st1 = S.stats()
+    res = S.align_scores(qq, k, w.width, S.SW)             # untimed: the result and its per-slot split
+    last = S.stats()
+    S.free_sequence(qq)
+    S.ssa_exit()
+    S.set_devices([])
+    S.set_device(job.dev_index)
+    cells = float(residues) * len(q)
+    step_ms = elapsed / steps * 1e3
+    n = max(1, st1["total_searches"] - st0["total_searches"])
+    skm, ssm = last["slot_kernel_ms"], last["slot_search_ms"]
+    slow = int(np.argmax(ssm)) if ssm else 0
+    rec = {
+        "workload": "SW int16 BLOSUM62 gaps -11/-1, 400-residue query (seed 7) vs the north-star DB, one process, "
+                    "sw_align on every slot (an unchanged libssa caller under SSA_AMD_DEVICES)",
+        "devices": devices, "slots": int(last["slots"]), "bit_width": 16, "steps": steps, "warmup": 1,
+        "db_seqs": seqs, "db_residues": residues, "cells_per_step": cells,
+        "ms_per_step": round(step_ms, 3), "value": round(cells / (elapsed / steps) / 1e9, 2), "unit": "GCUPS",
+        "kernel_ms_avg": round((st1["total_kernel_ms"] - st0["total_kernel_ms"]) / n, 4),
+        "slot_device": list(last["slot_device"]), "slot_kernel_ms": [round(x, 4) for x in skm],
+        "slot_search_ms": [round(x, 4) for x in ssm],
+        "step_split_ms": {"step": round(step_ms, 4), "slowest_slot": slow,
+                          "slot_kernel": round(skm[slow], 4) if skm else None,
+                          "slot_host": round(ssm[slow] - skm[slow], 4) if skm else None,
+                          "merge_and_rest": round(step_ms - ssm[slow], 4) if ssm else None},
+        "setup_s": round(setup_s, 1),
+        "top_hit": list(map(int, res[0][:2])) if res else None,
+    }
+    sh = argparse.Namespace(total=total, job_ids=job_ids, qlen=len(q))
+    m = fixture_match(w, sh, res, k, 1)
+    if m is not None:
+        rec["topk_vs_reference"] = m
+    job.dist.barrier()
+    return rec
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -748,6 +843,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
     job = Job(rank, world, dist, dev, backend)
+    job.dev_index = local
 
     import libssa_amd as S
 
@@ -790,6 +886,13 @@ def main():
     ns = None if args.no_north_star else north_star(S, args, job)
     if job.native:
         S.dist_finalize()
+    # --- the drop-in record (N > 1: one process on all N devices)
+    di = None
+    if world > 1 and not args.no_drop_in:
+        import torch
+        di = drop_in(S, args, job, torch.cuda.synchronize if dev == "cuda" else None)
+        if di is not None and ns is not None and ns.get("value"):
+            di["vs_multi_process"] = round(di["value"] / ns["value"], 4)
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -878,6 +981,8 @@ def main():
         out["cpu_baseline"] = cpu
     if ns is not None:
         out["north_star"] = ns
+    if di is not None:
+        out["drop_in"] = di
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

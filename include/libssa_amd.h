@@ -79,6 +79,11 @@ typedef struct {
                                 (option "rare_merge"; 0: none) */
     uint32_t rare_rescored;  /* entries holding one of them that the device filter forwarded and the
                                 int32 tier re-scored exactly */
+    uint32_t slots;          /* device slots of the last search (1: one device; more: SSA_AMD_DEVICES or
+                                ssa_amd_set_devices, one host thread per slot) */
+    int32_t slot_device[16];     /* per slot: its HIP device */
+    double slot_kernel_ms[16];   /* per slot: HIP-event time of its DP kernels */
+    double slot_search_ms[16];   /* per slot: host time of its device search and shard replay */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -86,15 +91,30 @@ typedef struct {
 #define SSA_AMD_TOPK 0      /* sorted top-k, as sw_align/nw_align */
 #define SSA_AMD_LOG 1       /* insertion log in replay order */
 
+/* Devices.  An unchanged libssa caller searches on every visible GPU, as
+ * the reference uses every core by default (src/util/thread_pool.c:42,
+ * get_nprocs()): at the first init_db, unless ssa_amd_set_device(s) was
+ * called before, the library reads the environment variable
+ *   SSA_AMD_DEVICES = all (also: unset or empty) | current | 0,2,...
+ * -- every visible device, the current HIP device only, or this list
+ * (repeats allowed: several slots on one device).  Several devices work as
+ * ssa_amd_set_devices below.  An explicit ssa_amd_set_device(s) always wins
+ * (one rank per GPU: ssa_amd_set_device(local_rank)). */
 int ssa_amd_device_count( void );
 void ssa_amd_set_device( int device );
 void ssa_amd_set_id_offset( size_t offset );
-/* Search on several devices from this one process (one host thread per
- * device inside sw_align / nw_align, the DB split into contiguous record
- * ranges at chunk_size boundaries, balanced by residues; results identical
- * to a single device).  n = 0 returns to single-device mode
- * (ssa_amd_set_device).  Returns 0, or 1 for an invalid device list. */
+/* Search on several devices from this one process (one persistent host
+ * thread per device slot inside sw_align / nw_align -- the caller's thread
+ * drives slot 0 -- the DB split into contiguous record ranges at chunk_size
+ * boundaries, balanced by residues, the slots' insertion logs merged in
+ * slot order; results identical to a single device).  n = 0 returns to
+ * single-device mode (ssa_amd_set_device).  Returns 0, or 1 for an invalid
+ * device list. */
 int ssa_amd_set_devices( const int * devices, int n );
+/* The device slots the next search uses (after SSA_AMD_DEVICES, which is
+ * read here if init_db has not read it yet): writes up to cap device ids to
+ * out (may be NULL) and returns the slot count. */
+int ssa_amd_get_devices( int * out, int cap );
 int ssa_amd_prepare_db( void );            /* pack + upload the DB now; returns 0 on success */
 void ssa_amd_get_stats( ssa_amd_stats_t * out );
 /* Tuning knobs (results never change, only which kernel computes them):

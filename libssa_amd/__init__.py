@@ -70,7 +70,9 @@ class ssa_amd_stats_t(Structure):
                 ("long_entries", c_uint32), ("long_kernel", ctypes.c_char * 24), ("part_retries", c_uint32),
                 ("total_searches", c_uint64), ("total_kernel_ms", c_double), ("total_search_ms", c_double),
                 ("filter_candidates", c_uint64), ("gather_ms", c_double), ("gather_rounds", c_uint32),
-                ("rare_merged", c_uint32), ("rare_rescored", c_uint32)]
+                ("rare_merged", c_uint32), ("rare_rescored", c_uint32), ("slots", c_uint32),
+                ("slot_device", ctypes.c_int32 * 16), ("slot_kernel_ms", c_double * 16),
+                ("slot_search_ms", c_double * 16)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24
@@ -88,7 +90,8 @@ EXPORTS = {
                       "ssa_amd_save_db", "ssa_amd_load_db", "ssa_amd_set_devices", "ssa_amd_search_batch",
                       "ssa_amd_dist_unique_id", "ssa_amd_dist_unique_id_bytes", "ssa_amd_dist_init",
                       "ssa_amd_dist_finalize", "ssa_amd_gather_logs", "ssa_amd_merge_logs", "ssa_amd_get_timeline",
-                      "ssa_amd_dist_available", "ssa_amd_dist_init_fake", "ssa_amd_dist_ranks", "ssa_amd_shard_bounds"],
+                      "ssa_amd_dist_available", "ssa_amd_dist_init_fake", "ssa_amd_dist_ranks", "ssa_amd_shard_bounds",
+                      "ssa_amd_get_devices"],
     "libssa_fasta_db.so": ["ssa_db_init", "ssa_db_get_sequence_count", "ssa_db_get_sequence", "ssa_db_close"],
 }
 
@@ -124,6 +127,7 @@ def load():
         "ssa_amd_query_views": ([P, POINTER(q_seq_t), c_size_t], c_size_t),
         "ssa_amd_save_db": ([c_char_p], c_int), "ssa_amd_load_db": ([c_char_p], c_int),
         "ssa_amd_set_devices": ([POINTER(c_int), c_int], c_int),
+        "ssa_amd_get_devices": ([POINTER(c_int), c_int], c_int),
         "ssa_amd_search_batch": ([POINTER(c_void_p), c_size_t, c_int, c_size_t, c_int, POINTER(ssa_hit_t),
                                   POINTER(c_size_t)], c_size_t),
         "ssa_amd_align_pair": ([c_int, c_char_p, c_size_t, c_char_p, c_size_t, POINTER(c_size_t), c_char_p, c_size_t],
@@ -239,6 +243,16 @@ def set_devices(devs):
     """ssa_amd_set_devices: search on all of `devs` from this process ([] = single device)."""
     arr = (c_int * max(len(devs), 1))(*devs)
     return load().ssa_amd_set_devices(arr, len(devs))
+
+
+def get_devices():
+    """ssa_amd_get_devices: the device slots the next search uses (after
+    SSA_AMD_DEVICES, read at the first init_db unless set_device(s) ran)."""
+    arr = (c_int * 16)()
+    n = load().ssa_amd_get_devices(arr, 16)
+    return [arr[i] for i in range(min(n, 16))]
+
+
 def set_id_offset(off): load().ssa_amd_set_id_offset(off)
 def prepare_db(): return load().ssa_amd_prepare_db()
 def set_option(name, value): load().ssa_amd_set_option(_b(name), value)
@@ -254,6 +268,9 @@ def stats():
     d = {f: getattr(s, f) for f, _ in ssa_amd_stats_t._fields_}
     d["kernel"] = d["kernel"].decode()
     d["long_kernel"] = d["long_kernel"].decode()
+    n = d["slots"]
+    for f in ("slot_device", "slot_kernel_ms", "slot_search_ms"):
+        d[f] = list(d[f])[:n]
     return d
 
 

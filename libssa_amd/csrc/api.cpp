@@ -2,6 +2,11 @@
 // reference's src/libssa.h:122-263, implemented in src/libssa.c) plus the
 // MI355X extensions of include/libssa_amd.h.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <numeric>
 #include <cmath>
 #include <cstdio>
@@ -19,6 +24,120 @@ p_query query_from_file(const char* path);
 }
 
 namespace {
+
+// SSA_AMD_DEVICES (include/libssa_amd.h), applied once -- at the first
+// init_db or device query -- unless the caller chose devices itself.  The
+// reference's default is every core (src/util/thread_pool.c:39-47); here it
+// is every visible GPU.
+void apply_device_env() {
+    Config& C = cfg();
+    if (C.device_chosen || C.device_env_read) return;
+    C.device_env_read = true;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return;                           // no device: the first search reports it
+    }
+    const char* e = getenv("SSA_AMD_DEVICES");
+    std::vector<int> devs;
+    if (!e || !*e || !strcmp(e, "all")) {
+        for (int i = 0; i < count && devs.size() < kMaxSlots; i++) devs.push_back(i);
+        if (devs.size() > 1) C.devices = devs;   // (one device: the current-device path, unchanged)
+        return;
+    }
+    if (!strcmp(e, "current")) return;
+    for (const char* p = e; *p;) {
+        char* end = nullptr;
+        const long d = strtol(p, &end, 10);
+        if (end == p || d < 0 || d >= count || devs.size() >= kMaxSlots) {
+            print_error("SSA_AMD_DEVICES=%s: not a list of at most %d of the %d visible devices; using the current "
+                        "device", e, (int)kMaxSlots, count);
+            return;
+        }
+        devs.push_back((int)d);
+        p = end;
+        if (*p == ',') p++;
+        else if (*p) {
+            print_error("SSA_AMD_DEVICES=%s: not a comma-separated device list; using the current device", e);
+            return;
+        }
+    }
+    if (devs.size() == 1) C.device = devs[0];
+    else if (devs.size() > 1) C.devices = devs;
+}
+
+// Persistent per-slot host threads for multi-device searches (SURVEY.md §8b
+// "one host thread per GPU inside sw_align"; the reference keeps its worker
+// pool across searches too, thread_pool.c:50-86).  run(n, fn) runs fn(0) on
+// the calling thread and fn(s) for 0 < s < n on worker s, and returns when
+// all are done.  A worker spins for a few ms after each job (a benchmark's
+// back-to-back searches hand over without a wake-up), then sleeps.  The pool
+// is never destroyed: its threads are detached and idle at process exit.
+class SlotPool {
+public:
+    void run(size_t n, const std::function<void(size_t)>& fn) {
+        if (n > 1) {
+            while (workers_ + 1 < n) {
+                const size_t s = ++workers_;
+                const uint64_t g0 = gen_.load(std::memory_order_acquire);
+                std::thread([this, s, g0]() { loop(s, g0); }).detach();
+            }
+            {
+                std::lock_guard<std::mutex> g(m_);
+                job_ = &fn;
+                njob_ = n;
+                pending_.store(n - 1, std::memory_order_relaxed);
+                gen_.fetch_add(1, std::memory_order_release);
+            }
+            cv_.notify_all();
+        }
+        fn(0);
+        while (n > 1 && pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    }
+
+private:
+    void loop(size_t s, uint64_t seen) {
+        using clk = std::chrono::steady_clock;
+        for (;;) {
+            const auto t0 = clk::now();
+            for (uint32_t it = 0; gen_.load(std::memory_order_acquire) == seen; it++) {
+                if ((it & 255) == 0 && clk::now() - t0 > std::chrono::milliseconds(5)) {
+                    std::unique_lock<std::mutex> lk(m_);
+                    cv_.wait(lk, [&]() { return gen_.load(std::memory_order_acquire) != seen; });
+                    break;
+                }
+                __builtin_ia32_pause();
+            }
+            // a consistent (generation, job) snapshot: run() writes both
+            // under the lock, and a job this worker belongs to is never
+            // replaced before the worker has finished it
+            const std::function<void(size_t)>* job;
+            size_t n;
+            {
+                std::lock_guard<std::mutex> g(m_);
+                seen = gen_.load(std::memory_order_acquire);
+                job = job_;
+                n = njob_;
+            }
+            if (s < n) {
+                (*job)(s);
+                pending_.fetch_sub(1, std::memory_order_acq_rel);
+            }
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<size_t> pending_{0};
+    const std::function<void(size_t)>* job_ = nullptr;
+    size_t njob_ = 0;
+    size_t workers_ = 0;                 // (grown by the caller's thread only)
+};
+
+SlotPool& slot_pool() {
+    static SlotPool* p = new SlotPool();   // (leaked on purpose: detached workers wait on it at exit)
+    return *p;
+}
 
 // test_configuration (libssa.c:196-219)
 void test_configuration(p_query q) {
@@ -90,10 +209,17 @@ struct SearchResult {
 // search that ran without the filter)
 uint64_t candidates(const SearchScores& x) { return x.sparse ? x.cand.size() : (uint64_t)x.entries * x.views; }
 
-void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPlan>& plan) {
+void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPlan>& plan,
+                   const std::vector<double>& slot_ms) {
     ssa_amd_stats_t& S = stats();
     S.kernel_ms = S.wide_ms = S.d2h_ms = S.prep_ms = S.upload_ms = S.sync_wait_ms = 0;
     S.cells = S.entries = S.wide_count = S.kernel_bytes = S.filter_candidates = 0;
+    S.slots = (uint32_t)std::min(sc.size(), (size_t)16);
+    for (size_t i = 0; i < 16; i++) {
+        S.slot_device[i] = i < S.slots ? plan[i].device : -1;
+        S.slot_kernel_ms[i] = i < S.slots ? sc[i].kernel_ms : 0;
+        S.slot_search_ms[i] = i < S.slots ? slot_ms[i] : 0;
+    }
     for (size_t i = 0; i < sc.size(); i++) {
         S.filter_candidates += candidates(sc[i]);
         // devices run concurrently: times are the slowest device's
@@ -131,20 +257,21 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     R.views = query_views(q);
     std::vector<SearchScores> sc(plan.size());
     std::vector<std::vector<Hit>> logs(plan.size());
+    std::vector<double> slot_ms(plan.size(), 0.0);
     if (plan.size() == 1) {
         device_search(device_db(0), R.views, algo, k, bw, sc[0]);
+        slot_ms[0] = now_ms() - t0;
     } else {
-        // one host thread per device; each replays its shard into a log of
-        // the elements its own heap accepts
-        std::vector<std::thread> pool;
-        for (size_t s = 0; s < plan.size(); s++)
-            pool.emplace_back([&, s]() {
-                check(hipSetDevice(plan[s].device), "hipSetDevice");
-                device_search(device_db(s), R.views, algo, k, bw, sc[s]);
-                TopK h(k);
-                replay(sc[s], device_db(s).meta, R.views, h, &logs[s]);
-            });
-        for (auto& t : pool) t.join();
+        // one persistent host thread per device slot (the caller's for slot
+        // 0); each replays its shard into a log of the elements its own heap
+        // accepts
+        slot_pool().run(plan.size(), [&](size_t s) {
+            const double ts = now_ms();
+            device_search(device_db(s), R.views, algo, k, bw, sc[s]);
+            TopK h(k);
+            replay(sc[s], device_db(s).meta, R.views, h, &logs[s]);
+            slot_ms[s] = now_ms() - ts;
+        });
     }
     const double t1 = now_ms();
     TopK heap(k);
@@ -164,7 +291,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
         o8 += x.dev_o8;
         o16 += x.dev_o16;
     }
-    publish_stats(sc, plan);
+    publish_stats(sc, plan, slot_ms);
     ssa_amd_stats_t& S = stats();
     S.overflow_8 = o8;
     S.overflow_16 = o16;
@@ -281,6 +408,7 @@ void init_symbol_translation(int type, int strands, int d_gencode, int q_gencode
 }
 
 void init_db(const char* db_file) {
+    apply_device_env();
     ssa_db_close();
     ssa_db_init(db_file);
     cfg().db_generation++;
@@ -319,10 +447,16 @@ void free_alignment(p_alignment_list alist) {
     free(alist);
 }
 
+// (libssa.c:266-271 frees the matrix, closes the DB and ends its thread
+// pool; here the device copies of the DB are released too)
 void ssa_exit(void) {
     matrix_free();
     ssa_db_close();
     cfg().db_generation++;
+    for (size_t s = 0; s < kMaxSlots; s++) {
+        DeviceDB& D = device_db(s);
+        if (D.device >= 0) D.release();
+    }
 }
 
 // ------------------------------------------------------------- extensions
@@ -335,11 +469,13 @@ int ssa_amd_device_count(void) {
 void ssa_amd_set_device(int device) {
     cfg().device = device;
     cfg().devices.clear();
+    cfg().device_chosen = true;
 }
 
 int ssa_amd_set_devices(const int* devices, int n) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    cfg().device_chosen = true;
     if (n <= 0 || !devices) {
         cfg().devices.clear();
         return 0;
@@ -355,6 +491,22 @@ int ssa_amd_set_devices(const int* devices, int n) {
         }
     cfg().devices.assign(devices, devices + n);
     return 0;
+}
+
+int ssa_amd_get_devices(int* out, int cap) {
+    apply_device_env();
+    const Config& C = cfg();
+    std::vector<int> d = C.devices;
+    if (d.size() <= 1) {
+        int dev = d.empty() ? C.device : d[0];
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            dev = -1;
+        }
+        d.assign(1, dev);
+    }
+    for (int i = 0; out && i < cap && i < (int)d.size(); i++) out[i] = d[i];
+    return (int)d.size();
 }
 void ssa_amd_set_id_offset(size_t offset) { cfg().id_offset = offset; }
 

@@ -28,6 +28,8 @@ struct Config {
     int8_t gap_open = 0, gap_extend = 0;  // libssa.c:35-36
     int device = -1;                      // -1: current HIP device
     std::vector<int> devices;             // ssa_amd_set_devices: shard the DB over these
+    bool device_chosen = false;           // the caller called ssa_amd_set_device(s): SSA_AMD_DEVICES is not read
+    bool device_env_read = false;         // SSA_AMD_DEVICES was applied (at the first init_db)
     size_t id_offset = 0;                 // global ID of local record 0
     uint64_t db_generation = 0;           // bumped by init_db
     // tuning knobs (ssa_amd_set_option)

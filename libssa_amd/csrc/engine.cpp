@@ -592,7 +592,7 @@ void ensure_device_db() {
 
 int save_packed_db(const char* path) {
     if (device_plan().size() != 1) {
-        print_error("Packed DB files are written from a single-device DB");
+        print_error("Packed DB files are written from a single-device DB (ssa_amd_set_device, or SSA_AMD_DEVICES=current)");
         return 1;
     }
     ensure_device_db();
@@ -650,7 +650,7 @@ int load_packed_db(const char* path) {
         return fail("packed for another symbol type / strands / genetic code");
     if (hdr64[0] != ssa_db_get_sequence_count()) return fail("record count differs from the open DB");
     const std::vector<SlotPlan> plan = device_plan();
-    if (plan.size() != 1) return fail("packed DB files load into a single device");
+    if (plan.size() != 1) return fail("packed DB files load into a single device (ssa_amd_set_device, or SSA_AMD_DEVICES=current)");
     const uint64_t E = hdr64[1], ng = hdr64[3];
     if (alpha[0] > 31 || E > ng * 64 || ng > E / 64 + 1) return fail("corrupt header");
     H.meta.records = hdr64[0];
@@ -1760,6 +1760,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // output, so the tier leaves the path from the pair kernel's end to
         // the result; the tables kernel then clears the filter header
         const bool side_tier = C.side_tier && rl32 > 0 && use_pair && out.sparse && !piped && !want_counts;
+        // (the host then waits for the stream's end, which covers the tier:
+        // a filter result handed straight to pinned memory would let the
+        // host read d_wide, and the tier's end event, before the tier ran)
+        if (side_tier) host_direct = false;
         // ... or after it, only when the search has overflowed lanes: the
         // filter forwards every overflowed lane (INT32_MIN) and leaves it out
         // of its bounds, so the tier's exact scores are needed only by the

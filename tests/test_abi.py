@@ -77,6 +77,36 @@ int main(void) {
         ["32", "24", "112", "72", "16", "24"]
 
 
+def test_stats_struct_layout_matches_ctypes(tmp_path):
+    """ssa_amd_stats_t as a C caller sees it (include/libssa_amd.h) and as
+    the Python mirror declares it: same size, same offsets of the last
+    fields (the per-slot arrays of the multi-device path)."""
+    src = tmp_path / "stats.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "libssa_amd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(ssa_amd_stats_t), offsetof(ssa_amd_stats_t, slots),
+         offsetof(ssa_amd_stats_t, slot_device), offsetof(ssa_amd_stats_t, slot_kernel_ms),
+         offsetof(ssa_amd_stats_t, slot_search_ms));
+  return 0;
+}''')
+    exe = tmp_path / "stats"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    T = S.ssa_amd_stats_t
+    assert got == [ctypes.sizeof(T), T.slots.offset, T.slot_device.offset, T.slot_kernel_ms.offset,
+                   T.slot_search_ms.offset]
+
+
+def test_device_query_without_gpu():
+    """ssa_amd_get_devices on a machine without a HIP device: one slot, the
+    current device unresolved (-1); nothing is fatal before a search."""
+    assert S.get_devices() in ([-1], [0])
+
+
 def test_reference_example_caller_links(tmp_path):
     """The reference's CLI (src/libssa_example.c) is the drop-in caller; a
     caller written against the same API links against libssa_amd.so."""

@@ -395,6 +395,96 @@ def _split_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
+class _FakeLib:
+    """The library calls bench.drop_in makes, recorded (no GPU): each search
+    'runs' on every selected slot; slot s takes (1 + s) ms of kernel."""
+    AMINOACID, NUCLEOTIDE, FORWARD_STRAND, MATRIX_BUILDIN, READ_FROM_STRING, SW = 0, 1, 1, 2, 1, 0
+
+    def __init__(self):
+        self.calls, self.devices, self.searches, self.records = [], [], 0, None
+
+    def __getattr__(self, name):        # configuration calls: recorded only
+        return lambda *a: self.calls.append((name,) + a)
+
+    def ssa_exit(self):
+        self.calls.append(("ssa_exit",))
+
+    def set_devices(self, devs):
+        self.calls.append(("set_devices", list(devs)))
+        self.devices = list(devs)
+        return 0
+
+    def init_db(self, path):
+        self.records = open(path).read().count(">")
+        self.calls.append(("init_db",))
+
+    def align_free(self, q, k, width, algo):
+        self.searches += 1
+
+    def align_scores(self, q, k, width, algo):
+        self.searches += 1
+        return [(100 - i, 7 * i) for i in range(k)]
+
+    def stats(self):
+        n = len(self.devices)
+        return {"total_searches": self.searches, "total_kernel_ms": float(n) * self.searches, "slots": n,
+                "slot_device": list(self.devices), "slot_kernel_ms": [1.0 + s for s in range(n)],
+                "slot_search_ms": [1.25 + s for s in range(n)]}
+
+
+def _dropin_worker(rank, world, port, outdir):
+    """One rank of bench.drop_in over gloo with the fake library."""
+    import argparse
+    import json
+    import sys
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(BENCH))
+    import bench
+    job = bench.Job(rank, world, dist, "cpu", "gloo")
+    job.dev_index = 0
+    args = argparse.Namespace(n_gpus=1, steps=4, north_star_steps=None, k=10, drop_in_seqs=3000, cpu_seconds=1.0)
+    lib = _FakeLib()
+    rec = bench.drop_in(lib, args, job)
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"rec": rec, "calls": [list(c[:1]) + [x for x in c[1:] if isinstance(x, (int, list))]
+                                         for c in lib.calls], "records": lib.records,
+                   "searches": lib.searches}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_drop_in_record_on_gloo_rehearsal(tmp_path, world):
+    """The N > 1 line's drop_in record (bench.drop_in): ranks != 0 release
+    their device DBs and wait; rank 0 opens the north-star DB (its first
+    3000 IDs here), selects one device slot per rank -- a rehearsal on one
+    GPU puts them all on device 0 -- times free_alignment(sw_align(...)) and
+    reports the per-slot kernel / search split; then it returns to its own
+    device."""
+    import json
+    mp.spawn(_dropin_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r0 = json.load(open(tmp_path / "rank0.json"))
+    d = r0["rec"]
+    assert d["devices"] == [0] * world and d["slots"] == world
+    assert d["db_seqs"] == 3000 and r0["records"] == 3000 and d["steps"] == 4
+    assert d["cells_per_step"] == d["db_residues"] * 400
+    assert d["slot_kernel_ms"] == [1.0 + s for s in range(world)]
+    assert d["slot_search_ms"] == [1.25 + s for s in range(world)]
+    sp = d["step_split_ms"]
+    assert sp["slowest_slot"] == world - 1 and sp["slot_kernel"] == world and sp["slot_host"] == 0.25
+    assert abs(sp["step"] - d["ms_per_step"]) < 1e-3 and d["value"] > 0
+    assert d["top_hit"] == [100, 0] and "topk_vs_reference" not in d      # (a 3000-ID slice: no fixture)
+    assert r0["searches"] == 4 + 2                                            # warm-up, 4 timed, the result
+    names = [c[0] for c in r0["calls"]]
+    assert names[0] == "ssa_exit" and ["set_devices", [0] * world] in r0["calls"]
+    assert r0["calls"][-2:] == [["set_devices", []], ["set_device", 0]]
+    for r in range(1, world):
+        rr = json.load(open(tmp_path / f"rank{r}.json"))
+        assert rr["rec"] is None and rr["calls"] == [["ssa_exit"]] and rr["searches"] == 0
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_bench_rank_split_explains_the_step(tmp_path, world):
     """The N > 1 bench line explains its own result (what the driver's first

@@ -816,6 +816,46 @@ def test_int32_rescore_tier_vs_oracle(algo, qlen, n):
     assert ms[0] > 0 and ms[1] > 0, ms
 
 
+def test_filter_host_with_side_tier_overflow():
+    """Options filter_host 1/2/3 (the filter's result in pinned memory) with
+    side_tier 1 (the int32 re-score tier beside the filter) on a DB whose
+    pair-kernel lanes overflow (SW maxima <= |R| are re-scored exactly: half
+    the entries share no residue with the query): the host must wait for
+    the tier before it reads the exact scores -- every combination equals
+    the oracle, and the timing read at the end never fails."""
+    rng = np.random.default_rng(23)
+    a, b = syn.AA_CODES[:10], syn.AA_CODES[10:]
+    q = rng.choice(a, size=300).astype(np.uint8)
+    n = 3000
+    lens = rng.integers(20, 400, n)
+    seqs = [rng.choice(b if i % 2 else syn.AA_CODES, size=int(x)).astype(np.uint8) for i, x in enumerate(lens)]
+    codes = np.concatenate(seqs)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    exp = po.scores(S.SW, q, codes, off, po.matrix_constant(5, -4), -3, -20)
+    ids = np.arange(n, dtype=np.uint64)
+    configure(False, ("const", 5, -4), -3, -20)
+    S.set_option("counters", 0)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, codes, off))
+        qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+        try:
+            for side in (1, 0):
+                S.set_option("side_tier", side)
+                for fh in (1, 2, 3, 0):
+                    S.set_option("filter_host", fh)
+                    for k in (1, 10, 64):
+                        got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+                        assert got == po.topk(exp, ids, k), (side, fh, k)
+                        st = S.stats()
+                        assert st["kernel"] == "pair_f16_sw" and st["wide_count"] >= n // 3, (side, fh, st["wide_count"])
+        finally:
+            S.set_option("side_tier", 0)
+            S.set_option("filter_host", 0)
+            S.set_option("counters", -1)
+        S.free_sequence(qq)
+
+
 def test_shard_logs_replay_to_global_result():
     """The insertion logs of consecutive ID shards, concatenated in shard
     order and replayed, equal the single-DB top-k including tie IDs."""
@@ -1559,6 +1599,83 @@ def test_reference_cli_links_and_matches(algo, bits):
     line = r.stdout.split("(Score, DB-ID), ")[1].splitlines()[0]
     got = [(int(a), int(b)) for a, b in re.findall(r"\((-?\d+), (\d+)\)", line)]
     assert got == [tuple(x) for x in case[algo.lower() + "_64"]]
+
+
+def _cli(db, query, algo, bits, k, devices):
+    import subprocess
+    env = dict(os.environ, SSA_AMD_DEVICES=devices)
+    r = subprocess.run([CLI, "-N", "4", "-O", "-11", "-E", "-1", "-M", "BLOSUM62", "-i", query, "-d", db,
+                        "-c", str(k), "-t", algo, "-b", str(bits), "-s", "AVX2"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, (devices, r.stderr[-2000:])
+    return r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="reference CLI not built (make -C oracle ref)")
+@pytest.mark.parametrize("algo", ["SW", "NW"])
+def test_reference_cli_on_several_devices_via_env(algo, tmp_path):
+    """An unchanged libssa caller on several GPUs: the reference's CLI
+    (src/libssa_example.c, compiled unchanged) with SSA_AMD_DEVICES=0,0,0
+    runs three device slots (here all on the box's one GPU: the same split,
+    per-slot packing, persistent slot threads and log merge as on three
+    GPUs) and prints exactly the single-device output -- every line but
+    m_run's per-worker bookkeeping lines, of which the reference too prints
+    one per worker thread (src/algo/manager.c:147-148).  Two DBs: AF091148
+    (1403 records, 2 chunks of the CLI's 1000: one slot is empty) and 5000
+    synthetic proteins (5 chunks)."""
+    codes, off = syn.protein_db(5000, 71, lo=1, hi=900)
+    big = _write_db(str(tmp_path), codes, off)
+    query = os.path.join(DATA, "Q3ZAI3.fasta")
+    for db, k in ((os.path.join(DATA, "AF091148.fas"), 300), (big, 500)):
+        for bits in (8, 16):
+            one = _cli(db, query, algo, bits, k, "current")
+            three = _cli(db, query, algo, bits, k, "0,0,0")
+
+            def split(out):
+                book = [ln for ln in out.splitlines() if "Processed chunks" in ln]
+                return [ln for ln in out.splitlines() if "Processed chunks" not in ln], book
+            body1, book1 = split(one)
+            body3, book3 = split(three)
+            assert body1 == body3, (db, bits)
+            assert f"Nr of alignments: {k}" in one
+            assert len(book1) == 1 and len(book3) == 3, (book1, book3)
+            seqs = [int(ln.rsplit(" ", 1)[1]) for ln in book3]
+            assert sum(seqs) == int(book1[0].rsplit(" ", 1)[1]), (book1, book3)
+
+
+def test_device_env_selects_slots(tmp_path):
+    """SSA_AMD_DEVICES, read at the first init_db unless the caller chose
+    devices: all / unset / empty = every visible device, current = the
+    current one, a list (repeats allowed), invalid lists fall back to the
+    current device with an error; an explicit ssa_amd_set_device wins."""
+    import subprocess
+    import sys
+    db = os.path.join(DATA, "test.fas")
+    prog = ("import sys; sys.path.insert(0, %r); import libssa_amd as S; S.load(); "
+            "S.set_output_mode(S.OUTPUT_ERROR); " % ROOT)
+    n = S.device_count()
+
+    def devs(env, pre=""):
+        e = dict(os.environ)
+        e.pop("SSA_AMD_DEVICES", None)
+        if env is not None:
+            e["SSA_AMD_DEVICES"] = env
+        r = subprocess.run([sys.executable, "-c", prog + pre + f"S.init_db({db!r}); print(S.get_devices())"],
+                           capture_output=True, text=True, timeout=300, env=e)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return eval(r.stdout.strip().splitlines()[-1]), r.stdout
+    allv = list(range(n)) if n > 1 else [0]
+    assert devs(None)[0] == allv
+    assert devs("")[0] == allv
+    assert devs("all")[0] == allv
+    assert devs("current")[0] == [0]
+    assert devs("0,0,0")[0] == [0, 0, 0]
+    assert devs("0")[0] == [0]
+    for bad in ("0,99", "x", "0;1", "-1"):
+        got, out = devs(bad)
+        assert got == [0] and "SSA_AMD_DEVICES" in out, (bad, got, out)
+    assert devs("0,0", pre="S.set_device(0); ")[0] == [0]
+    assert devs("current", pre="S.set_devices([0, 0]); ")[0] == [0, 0]
 
 
 @pytest.mark.parametrize("gaps", [(0, 0), (-5, 0), (0, -1), (-1, -3), (-20, -7)])

@@ -2,7 +2,7 @@
 """Where the time between two searches goes: the HIP API calls, kernels and
 copies from one pair_kernel's end to the next one's start, from a
 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace run
-(tools/r4_runs.sh api_trace).  usage: api_gap.py <trace dir> [which gap, default -2]"""
+(tools/runs.sh api_trace).  usage: api_gap.py <trace dir> [which gap, default -2]"""
 import csv
 import glob
 import os

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The gap between consecutive pair launches cut at the device events inside
 it (medians over every gap of a rocprofv3 --kernel-trace --memory-copy-trace
-run, tools/r5_runs.sh kgap): pair end -> filter_block start (the long-stream
+run, tools/runs.sh kgap): pair end -> filter_block start (the long-stream
 joins and the kernel-end marker), the filter chain, the result copy, copy end
 -> next upload start (host: result, return, next call, plan, launches), upload,
 upload end -> tables start, tables, tables end -> pair start.
