@@ -61,27 +61,13 @@ CONFIGS = W.CONFIGS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-# VALU instructions per cell of each scoring kernel (all its launches of a
-# search), from PMC SQ_INSTS_VALU x 64 lanes / cells over the C2 (SW) and C3
-# (NW) searches: profiles/r01/pmc_c2_sw_np16 (strip16), pmc_c2_r01b and
-# pmc_c3_r01b (32-row pair strips), pmc_c2_np24 / pmc_c3_np24 (48-row strips),
-# pmc_c2_rel / pmc_c3_rel (48-row strips, diagonal-relative values),
-# pmc_c2_r01d / pmc_c3_r01d (SW running maximum along anti-diagonals),
-# pmc_c2_r01e / pmc_c3_r01e (+ first-strip boundary from memory),
-# pmc_{c2,c3,c5,ref}_r01g (+ diagonal add as v_add_u32, long_kernel),
-# profiles/r02/pmc_c2_s3 (48-row SW strips, the default, 24-bit LDS address),
-# profiles/r02/pmc_c3_np40 (80-row NW strips, the default) and
-# profiles/r03/pmc_c2 (round 3: strip parts, long16_kernel; 6.654e9 x 64 /
-# 1.406e11 = 3.03) and profiles/r03/final/pmc_c2 / pmc_c3 (round 3: the
-# pair-row stream; SW 6.444e9 x 64 / 1.406e11 = 2.93, NW 80-row 1.439e10 x
-# 64 / 3.516e11 = 2.62) and round 4 (16-bit pair-row stream: profiles/r04/
-# pmc_final/c2 SW 6.489e9 x 64 / 1.406e11 = 2.95, profiles/r04/pmc/c3 NW
-# 1.435e10 x 64 / 3.516e11 = 2.61) and round 5 (row-drop table, SW floors in
-# one SGPR: profiles/r05/pmc_final2/c2 2.962, profiles/r05/pmc_final/c3 2.627).
-# Keyed by (kernel, pair strip rows): the instruction count per cell depends
-# on the strip height.
-VALU_INSTR_PER_CELL = {("strip16_sw", 0): 5.59, ("strip_f16m_sw", 0): 4.79, ("pair_f16_sw", 48): 2.96,
-                       ("pair_f16_nw", 48): 2.74, ("pair_f16_nw", 80): 2.63}
+# The VALU issue roofline's inputs -- VALU lane-instructions per cell over a
+# search's DP kernels and the effective clock -- are PMC measurements of the
+# exact build and workload (tools/profile_pmc.sh -> tools/traffic_from_pmc.py
+# -> profiles/traffic.json, filed under the workload key and the kernel-source
+# hash, libssa_amd/workloads.py kernel_src_hash); a line whose build hashes
+# differently reports them null with roofline.traffic_stale (rounds 1-5 kept
+# them in constant tables here: profiles/r0*/pmc_*).
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
 # profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
@@ -907,21 +893,20 @@ def main():
     alg_bytes = float(st["kernel_bytes"])
     achieved = alg_bytes / (kavg * 1e-3) / 1e9
     tkey = traffic_key(w, sh, st)
-    traffic, tsrc = None, None
-    tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf):
-        rec = json.load(open(tf)).get(tkey)
-        if rec:
-            traffic, tsrc = rec["bytes_per_launch"], rec["source"]
+    src_hash = W.kernel_src_hash()
+    pf = W.profiled_figures(tkey, src_hash, os.path.join(ROOT, "profiles", "traffic.json"))
+    traffic, tsrc = pf["traffic"], pf["source"]
     # VALU issue roofline: VOP3/VOP3P instructions issue at
     # 4.17 cycles per wave64 instruction per SIMD, v_add_u32 at 2.5 (measured
     # in isolation: profiles/r01/ubench_valu_rates4.txt); instructions per
-    # cell from PMC SQ_INSTS_VALU (profiles/r01/pmc_{c2,c3,c5}_r01g).
+    # cell and the clock from this build's PMC pass of this workload
     kkey = (st["kernel"], st["strip_rows"])
-    instr_per_cell = VALU_INSTR_PER_CELL.get(kkey) if args.strip_np == 16 else None
+    instr_per_cell, clock = pf["valu_instr_per_cell"], pf["clock_ghz"]
+    if args.strip_np != 16:
+        instr_per_cell = None
     fast = VALU_FAST_SHARE.get(kkey, 0.0)
     issue_cycles = (1.0 - fast) * 4.17 + fast * 2.5
-    valu_bound = (1024 * 2.4e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
+    valu_bound = (1024 * clock * 1e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell and clock else None
     out = {
         "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
         "value": round(gcups, 2),
@@ -944,11 +929,13 @@ def main():
                    "strip_np": args.strip_np, "bit_width": w.width},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_key": tkey,
-                     "traffic_source": tsrc,
+                     "traffic_source": tsrc, "kernel_src": src_hash, "traffic_stale": pf["stale"],
+                     **({"traffic_stale_source": pf["stale_source"]} if pf.get("stale_source") else {}),
                      # the resource that actually binds this integer DP
                      "binding": {"bound": "valu_issue",
                                  "achieved": round(cells_local / (kavg * 1e-3) / 1e9, 2),
                                  "peak": round(valu_bound / 1e9, 1) if valu_bound else None, "unit": "GCUPS",
+                                 "clock_ghz": clock, "valu_instr_per_cell": instr_per_cell,
                                  "frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None}},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),

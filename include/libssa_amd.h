@@ -178,7 +178,12 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        published by the end of the dispatch, the host synchronising as usual)
  *   "sync_spin" 1|0      1 (default): the host thread spins while a search runs (hipDeviceScheduleSpin,
  *                        set at the library's first pack on a device; 15 us less between two
- *                        searches); 0: HIP's own scheduling (yields the core)
+ *                        searches); 0: HIP's own scheduling (yields the core).  The flag is
+ *                        PROCESS-WIDE for that device: every HIP user of the process (e.g. torch)
+ *                        then spins in its own synchronisations too, and a search keeps one host
+ *                        core busy for its whole duration.  It only takes effect when the library
+ *                        is the first to use the device in the process (a context made before keeps
+ *                        its flags); set 0 before the first init_db to leave the flags alone
  *   "lean_events" 1|0    1 (default): no timing markers around the upload, the re-score tier
  *                        and the filter (stats upload_ms, wide_ms, d2h_ms read 0; kernel_ms
  *                        kept; C2 +0.5 %, profiles/r05/ab/lean_events); 0: all markers

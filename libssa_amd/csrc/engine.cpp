@@ -401,6 +401,12 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         // of the device; a context another runtime user made first keeps its
         // flags (the call's error is cleared)
         if (C.sync_spin && hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
+        // the code object holds gfx950 kernels only, and the launch plans use
+        // gfx950's measured LDS allocation rule (kernels.h pair_wgs_per_cu)
+        hipDeviceProp_t prop;
+        check(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            fatal("libssa_amd is built for gfx950 (MI355X) only; device %d is %s", dev, prop.gcnArchName);
         check(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking), "hipStreamCreate");
         // the long-entry kernels' streams at the device's highest priority:
         // their workgroups are the search's critical path (see also the gate,

@@ -23,7 +23,10 @@ __host__ __device__ constexpr uint32_t pair_lds_row(uint32_t A, uint32_t c1, uin
 // Workgroups of `bytes` dynamic LDS that one gfx950 CU keeps resident (LDS
 // alone): allocations are rounded up to 1 280 B (measured, tools/ubench/
 // lds_occ.hip, profiles/r05/lds_occ.txt: 40 960 B -> 4, 53 760 B -> 3,
-// 54 208 B -> 2, 75 776 B -> 2 -- 160 KiB / 3 = 54 613 B is not reachable)
+// 54 208 B -> 2, 75 776 B -> 2 -- 160 KiB / 3 = 54 613 B is not reachable).
+// gfx950's granule: the library holds gfx950 code only and refuses any other
+// device at its first use of it (engine.cpp upload_pack), so the plan never
+// meets another architecture's allocation rule.
 constexpr size_t kLdsGranule = 1280;
 constexpr size_t pair_wgs_per_cu(size_t bytes) {
     return bytes == 0 ? 4 : kPairLdsMax / ((bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule);

@@ -115,3 +115,44 @@ def rank_layout(world: int, ngpu: int, local: int, backend: str):
         raise SystemExit(f"{world} ranks but only {ngpu} GPU(s) visible (a rehearsal needs SSA_DIST_BACKEND=gloo)")
     n = max(1, ngpu)
     return local % n, -(-world // n), n
+
+
+# The DP kernels' sources: a PMC-derived figure (HBM traffic, VALU
+# instructions per cell, clock) describes the build it was measured on, so
+# profiles/traffic.json files each record under this hash and bench.py reports
+# it only while the sources still hash the same (roofline.traffic_stale).
+KERNEL_SOURCES = ("libssa_amd/csrc/pair_kernel.h", "libssa_amd/csrc/kernels.hip", "libssa_amd/csrc/dp_common.h",
+                  "libssa_amd/csrc/kernels.h", "libssa_amd/csrc/pair_sw.hip", "libssa_amd/csrc/pair_nw.hip")
+
+
+def kernel_src_hash(root: str = ROOT) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def profiled_figures(key: str, src_hash: str, path: str) -> dict:
+    """The PMC figures profiles/traffic.json holds for workload `key`, if
+    they were measured on kernel sources hashing to `src_hash`:
+    {"traffic", "source", "valu_instr_per_cell", "clock_ghz", "stale"} --
+    stale True (and every figure None) when the record belongs to another
+    build, None when there is no record for the workload."""
+    import json
+    out = {"traffic": None, "source": None, "valu_instr_per_cell": None, "clock_ghz": None, "stale": None}
+    if not os.path.exists(path):
+        return out
+    rec = json.load(open(path)).get(key)
+    if not rec:
+        return out
+    if rec.get("kernel_src") != src_hash:
+        out["stale"] = True
+        out["stale_source"] = rec.get("source")
+        return out
+    out.update(traffic=rec["bytes_per_launch"], source=rec["source"], stale=False,
+               valu_instr_per_cell=rec.get("valu_instr_per_cell"), clock_ghz=rec.get("clock_ghz"))
+    return out

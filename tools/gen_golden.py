@@ -318,6 +318,14 @@ FULLSIZE = {
     "sprot": dict(kind="protein", n=548_208, i1=548_208, seed=42, qlen=513, query_file="tests/golden/data/P18080.fasta",
                   matrix="blosum50", gap_open=-3, gap_extend=-1, algo="sw", width=16, alphabet="sprot25",
                   tail=300, tail_seed=77),
+    # round 6: the two bench_all shapes that had no fixture -- the reference's
+    # benchmark shape in 20 letters (bench.py --config ref: P18080 vs 548 208
+    # sequences, BLOSUM50 -3/-1) and C2's DB in the reference generator's
+    # uniform 28 symbols at its full 1 M (bench.py --alphabet uniform28)
+    "ref": dict(kind="protein", n=548_208, i1=548_208, seed=42, qlen=513, query_file="tests/golden/data/P18080.fasta",
+                matrix="blosum50", gap_open=-3, gap_extend=-1, algo="sw", width=16, alphabet="bg20"),
+    "u28c2": dict(kind="protein", n=1_000_000, i1=1_000_000, seed=42, qlen=400, qseed=7, matrix="blosum62",
+                  gap_open=-11, gap_extend=-1, algo="sw", width=16, alphabet="uniform28"),
 }
 
 

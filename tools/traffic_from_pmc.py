@@ -1,46 +1,96 @@
 #!/usr/bin/env python3
-"""Turns a tools/profile_pmc.sh output directory into the per-launch HBM
-traffic figure bench.py reports as roofline.traffic (profiles/traffic.json).
+"""Turns a tools/profile_pmc.sh output directory into the per-workload
+figures bench.py reports (profiles/traffic.json):
 
-Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly half
-the bytes of a wide coalesced streaming read on gfx950 -> x2; WRITE_SIZE is
-exact for 16-B-per-lane streaming stores.  Both kernels' loads and stores are
-16 B per lane, fully coalesced."""
+  bytes_per_launch     roofline.traffic: HBM bytes of one dominant-kernel launch
+  valu_instr_per_cell  VALU lane-instructions per cell over every DP kernel of a
+                       search (pair + long-entry kernels), from the valu pass
+  clock_ghz            the pair kernel's effective clock in that pass
+                       (GRBM_GUI_ACTIVE / 8 XCDs / duration)
+  kernel_src           the kernel-source hash the profiled bench line printed
+                       (roofline.kernel_src): bench.py reports the figures only
+                       while its own build hashes the same
+
+HBM correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly
+half the bytes of a wide coalesced streaming read on gfx950 -> x2; WRITE_SIZE
+is exact for 16-B-per-lane streaming stores.  Both kernels' loads and stores
+are 16 B per lane, fully coalesced.  Every figure skips each kernel's first
+(warm-up) dispatch."""
+import collections
 import csv
 import json
 import os
 import sys
 
 
-def mean_counter(d, name, kernel=None):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
-            if r["Counter_Name"] == name and (kernel is None or kernel in r["Kernel_Name"])]
-    return sum(vals) / len(vals)
+def per_dispatch(path):
+    """{kernel: [{counter: value, "_ns": duration}, ...]} of one pass, in dispatch order."""
+    rows = collections.defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        key = (r["Dispatch_Id"], r["Kernel_Name"])
+        rows[key][r["Counter_Name"]] = float(r["Counter_Value"])
+        rows[key]["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    out = collections.defaultdict(list)
+    for (_, k), v in sorted(rows.items(), key=lambda x: int(x[0][0])):
+        out[k].append(v)
+    return out
 
 
-def bench_key(pmc_dir):
-    """The workload key bench.py printed (roofline.traffic_key) in the PMC
-    pass's own log: the traffic is filed under the exact workload profiled."""
-    for name in ("fetch.log", "write.log", "stats.log"):
+def mean(x):
+    return sum(x) / len(x) if x else None
+
+
+def kernel_mean(d, name, kernel):
+    """Mean of a counter over the matching kernel's dispatches after its first."""
+    pd = per_dispatch(os.path.join(d, "run_counter_collection.csv"))
+    vals = [x[name] for k, xs in pd.items() if kernel is None or kernel in k for x in xs[1:] if name in x]
+    return mean(vals)
+
+
+def bench_line(pmc_dir):
+    """The bench.py line of the pass's own log: the workload key and the
+    kernel-source hash the figures are filed under."""
+    for name in ("fetch.log", "write.log", "valu.log", "stats.log"):
         p = os.path.join(pmc_dir, name)
         if os.path.exists(p):
             for line in reversed(open(p).read().splitlines()):
                 if line.startswith("{"):
-                    return json.loads(line)["roofline"]["traffic_key"]
+                    return json.loads(line)
     raise SystemExit(f"no bench.py line under {pmc_dir}")
+
+
+def is_dp(k):
+    return "pair_kernel<" in k or "long16_kernel<" in k or "long_kernel<" in k or "strip" in k
+
+
+def valu_figures(pmc_dir, cells):
+    path = os.path.join(pmc_dir, "valu", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        return None, None
+    pd = per_dispatch(path)
+    pair = [x for k, xs in pd.items() if "pair_kernel<" in k for x in xs[1:]]
+    clock = mean([x["GRBM_GUI_ACTIVE"] / 8 / x["_ns"] for x in pair]) if pair else None
+    dp = sum(mean([x["SQ_INSTS_VALU"] for x in xs[1:]]) or 0.0 for k, xs in pd.items() if is_dp(k))
+    return dp * 64 / cells, clock
 
 
 def main():
     # usage: traffic_from_pmc.py <profile_pmc.sh out dir> [kernel name substring]
     pmc_dir = sys.argv[1]
-    key = bench_key(pmc_dir)
-    kernel = sys.argv[2] if len(sys.argv) > 2 else None   # substring of the dominant kernel's name
-    fetch = mean_counter(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE", kernel) * 1024 * 2
-    write = mean_counter(os.path.join(pmc_dir, "write"), "WRITE_SIZE", kernel) * 1024
+    line = bench_line(pmc_dir)
+    key = line["roofline"]["traffic_key"]
+    src = line["roofline"].get("kernel_src")
+    if not src:
+        raise SystemExit(f"{pmc_dir}: the bench line predates roofline.kernel_src; profile again")
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "pair_kernel"
+    fetch = kernel_mean(os.path.join(pmc_dir, "fetch"), "FETCH_SIZE", kernel) * 1024 * 2
+    write = kernel_mean(os.path.join(pmc_dir, "write"), "WRITE_SIZE", kernel) * 1024
+    vpc, clock = valu_figures(pmc_dir, line["config"]["cells_per_step"])
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "profiles", "traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[key] = {"bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
+                 "valu_instr_per_cell": vpc, "clock_ghz": clock, "kernel_src": src,
                  "source": os.path.relpath(pmc_dir, root), "kernel": kernel}
     json.dump(data, open(path, "w"), indent=1)
     print(key, data[key])
