@@ -789,10 +789,13 @@ def drop_in(S, args, job, torch_sync=None):
         "kernel_ms_avg": round((st1["total_kernel_ms"] - st0["total_kernel_ms"]) / n, 4),
         "slot_device": list(last["slot_device"]), "slot_kernel_ms": [round(x, 4) for x in skm],
         "slot_search_ms": [round(x, 4) for x in ssm],
-        "step_split_ms": {"step": round(step_ms, 4), "slowest_slot": slow,
+        # (the split of one search, the untimed one after the loop: its
+        # slowest slot's kernel and host time, then the merge of the slot logs
+        # and the rest of the call)
+        "step_split_ms": {"step": round(step_ms, 4), "search": round(last["search_ms"], 4), "slowest_slot": slow,
                           "slot_kernel": round(skm[slow], 4) if skm else None,
                           "slot_host": round(ssm[slow] - skm[slow], 4) if skm else None,
-                          "merge_and_rest": round(step_ms - ssm[slow], 4) if ssm else None},
+                          "merge_and_rest": round(last["search_ms"] - ssm[slow], 4) if ssm else None},
         "setup_s": round(setup_s, 1),
         "top_hit": list(map(int, res[0][:2])) if res else None,
     }

@@ -84,6 +84,8 @@ typedef struct {
     int32_t slot_device[16];     /* per slot: its HIP device */
     double slot_kernel_ms[16];   /* per slot: HIP-event time of its DP kernels */
     double slot_search_ms[16];   /* per slot: host time of its device search and shard replay */
+    uint32_t graph;          /* slot 0's last search: 0 issued call by call, 1 captured into a new HIP graph,
+                                2 replayed the cached graph (option "graph") */
 } ssa_amd_stats_t;
 
 #define SSA_AMD_SW 0
@@ -138,6 +140,10 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
  *                        merges at the list width k needs, for DBs of <= 256 filter blocks
  *                        (default), or always the general scan
+ *   "graph" 1|0          1 (default): a single-view search with the device filter and no overflow
+ *                        counters runs as a cached HIP graph -- captured once per launch plan, replayed
+ *                        with the changed kernel arguments set on their nodes (stats graph); 0: every
+ *                        stream operation issued on its own
  *   "upload_kernel" 1|0  1 (default): the per-search upload block (matrix, boundary, query) is read
  *                        from pinned host memory by a kernel on the search's stream; 0: a
  *                        copy-engine transfer (hipMemcpyAsync)

@@ -72,7 +72,7 @@ class ssa_amd_stats_t(Structure):
                 ("filter_candidates", c_uint64), ("gather_ms", c_double), ("gather_rounds", c_uint32),
                 ("rare_merged", c_uint32), ("rare_rescored", c_uint32), ("slots", c_uint32),
                 ("slot_device", ctypes.c_int32 * 16), ("slot_kernel_ms", c_double * 16),
-                ("slot_search_ms", c_double * 16)]
+                ("slot_search_ms", c_double * 16), ("graph", c_uint32)]
 
 
 assert ctypes.sizeof(db_seq_t) == 32 and ctypes.sizeof(q_seq_t) == 24

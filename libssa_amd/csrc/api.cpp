@@ -215,6 +215,7 @@ void publish_stats(const std::vector<SearchScores>& sc, const std::vector<SlotPl
     S.kernel_ms = S.wide_ms = S.d2h_ms = S.prep_ms = S.upload_ms = S.sync_wait_ms = 0;
     S.cells = S.entries = S.wide_count = S.kernel_bytes = S.filter_candidates = 0;
     S.slots = (uint32_t)std::min(sc.size(), (size_t)16);
+    S.graph = sc.empty() ? 0u : sc[0].graph;
     for (size_t i = 0; i < 16; i++) {
         S.slot_device[i] = i < S.slots ? plan[i].device : -1;
         S.slot_kernel_ms[i] = i < S.slots ? sc[i].kernel_ms : 0;
@@ -607,6 +608,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "tail_rows4")) cfg().tail_rows4 = (int)value;
     else if (!strcmp(name, "tier_defer")) cfg().tier_defer = (int)value;
     else if (!strcmp(name, "upload_kernel")) cfg().upload_kernel = (int)value;
+    else if (!strcmp(name, "graph")) cfg().graph = (int)value;
     else if (!strcmp(name, "filter_prefix_regs")) set_filter_prefix_regs((int)value);
     else print_warning("unknown option %s", name);
 }

@@ -406,18 +406,18 @@ hipError_t launch_flags(const FlagArgs& a, hipStream_t st) {
     if (a.nlanes == 0) return hipSuccess;
     hipError_t e = hipSuccess;
     if (!a.lists_zeroed) {
-        if ((e = hipMemsetAsync(a.list, 0, 4, st)) != hipSuccess) return e;
-        if (a.rlist && (e = hipMemsetAsync(a.rlist, 0, 4, st)) != hipSuccess) return e;
+        if ((e = op_set(a.list, 0, 4, st)) != hipSuccess) return e;
+        if (a.rlist && (e = op_set(a.rlist, 0, 4, st)) != hipSuccess) return e;
     }
-    if (a.entries > 0) hipLaunchKernelGGL(flags_decide_kernel, dim3((a.entries + 255) / 256), dim3(256), 0, st, a);
-    if (a.m > 0) hipLaunchKernelGGL(flags_replay_kernel, dim3(a.threads / 64), dim3(64), 0, st, a);
-    if (a.m > 0 && a.rlist) hipLaunchKernelGGL(flags_replay_rows_kernel, dim3(a.rthreads / 64), dim3(64), 0, st, a);
+    if (a.entries > 0) (void)ssa_launch((const void*)&flags_decide_kernel, dim3((a.entries + 255) / 256), dim3(256), 0, st, a);
+    if (a.m > 0) (void)ssa_launch((const void*)&flags_replay_kernel, dim3(a.threads / 64), dim3(64), 0, st, a);
+    if (a.m > 0 && a.rlist) (void)ssa_launch((const void*)&flags_replay_rows_kernel, dim3(a.rthreads / 64), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 
 hipError_t launch_count(const CountArgs& a, hipStream_t st) {
     if (a.entries == 0) return hipSuccess;
-    hipLaunchKernelGGL(count_kernel, dim3((a.entries + 255) / 256), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&count_kernel, dim3((a.entries + 255) / 256), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

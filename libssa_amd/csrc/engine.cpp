@@ -45,10 +45,22 @@ static void dfree(void* p) {
     if (p) (void)hipFree(p);
 }
 
+void DeviceDB::SearchGraph::reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (g) (void)hipGraphDestroy(g);
+    exec = nullptr;
+    g = nullptr;
+    ops.clear();
+    nodes.clear();
+}
+
 void DeviceDB::release() {
     // the buffers belong to `device`: free them there (a failure here means
     // the device is gone -- fatal, as every other HIP error of the library)
     if (device >= 0) check(hipSetDevice(device), "hipSetDevice");
+    // (the cached graph names the buffers freed below)
+    graph.reset();
+    graph.broken = false;
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch); dfree(d_rscratch);
@@ -423,6 +435,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         // device-scope release, not a system-scope one (an L2 writeback of
         // the search's row-buffer lines each time, ~5 us on the path)
         for (auto& e : D.ev) check(hipEventCreateWithFlags(&e, kEventFlags), "hipEventCreate");
+        check(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming), "hipEventCreate");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
             D.nsimd = (uint32_t)cus * 4;
@@ -1228,6 +1241,127 @@ static void ensure_entry_masks(DeviceDB& D) {
         for (; x; x &= x - 1) D.code_entries[__builtin_ctz(x)]++;
 }
 
+// ---------------------------------------------------------- search graph
+// A search's stream operations, recorded (launch.h), are replayed as one
+// HIP graph: the cached graph when the operations have the same shape as
+// the ones it was captured from (kinds, streams, kernels, grids, events,
+// argument sizes), with every changed argument block or copy set on its node
+// (hipGraphExecKernelNodeSetParams: the tables kernel's gate target, the pair
+// kernel's strip-part epoch, the candidate copy's length change per search);
+// otherwise the operations are captured into a new graph.  One graph launch
+// instead of ~12 calls: less host issue time and fewer barrier packets
+// between the kernels (tools/graph_probe.hip).
+static bool same_shape(const StreamOp& a, const StreamOp& b) {
+    if (a.kind != b.kind || a.stream != b.stream) return false;
+    switch (a.kind) {
+    case StreamOp::kKernel:
+        return a.func == b.func && a.grid.x == b.grid.x && a.grid.y == b.grid.y && a.grid.z == b.grid.z &&
+               a.block.x == b.block.x && a.block.y == b.block.y && a.block.z == b.block.z && a.lds == b.lds &&
+               a.args.size() == b.args.size() && a.arg_off == b.arg_off;
+    case StreamOp::kCopy:
+        return a.ck == b.ck;
+    case StreamOp::kSet:
+        return a.dst == b.dst && a.value == b.value && a.bytes == b.bytes;
+    case StreamOp::kRecord:
+        return a.event == b.event && a.timing == b.timing;
+    case StreamOp::kWait:
+        return a.event == b.event;
+    }
+    return false;
+}
+
+static void issue_all(const std::vector<StreamOp>& ops) {
+    for (const StreamOp& op : ops) check(issue_op(op, false), "stream operation");
+}
+
+// A sync point inside the recording window: what was recorded is issued as
+// it stands and the rest of the search runs call by call.
+static void sync_point(hipStream_t s, const char* what) {
+    if (OpRecorder* r = op_recorder()) {
+        op_recorder() = nullptr;
+        issue_all(r->ops);
+        r->ops.clear();
+    }
+    check(hipStreamSynchronize(s), what);
+}
+
+static bool capture_ops(DeviceDB::SearchGraph& G, const std::vector<StreamOp>& ops, hipStream_t st) {
+    G.reset();
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+    std::vector<hipGraphNode_t> nodes(ops.size(), nullptr);
+    bool ok = true;
+    for (size_t i = 0; i < ops.size() && ok; i++) {
+        const StreamOp& op = ops[i];
+        ok = issue_op(op, true) == hipSuccess;
+        if (ok && (op.kind == StreamOp::kKernel || op.kind == StreamOp::kCopy || op.kind == StreamOp::kSet)) {
+            hipStreamCaptureStatus cs;
+            const hipGraphNode_t* deps = nullptr;
+            size_t nd = 0;
+            ok = hipStreamGetCaptureInfo_v2(op.stream, &cs, nullptr, nullptr, &deps, &nd) == hipSuccess &&
+                 cs == hipStreamCaptureStatusActive && nd == 1;
+            if (ok) nodes[i] = deps[0];
+        }
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &g);
+    ok = ok && e == hipSuccess && g;
+    if (ok) ok = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0) == hipSuccess;
+    if (!ok) {
+        if (g) (void)hipGraphDestroy(g);
+        G.exec = nullptr;
+        (void)hipGetLastError();
+        return false;
+    }
+    G.g = g;
+    G.ops = ops;
+    G.nodes = std::move(nodes);
+    G.captures++;
+    return true;
+}
+
+// returns 0: issued call by call, 1: captured, 2: replayed
+static uint32_t run_ops(DeviceDB& D, OpRecorder& rec, hipStream_t st) {
+    DeviceDB::SearchGraph& G = D.graph;
+    const std::vector<StreamOp>& ops = rec.ops;
+    if (ops.empty()) return 0;
+    bool same = G.exec && G.ops.size() == ops.size();
+    for (size_t i = 0; same && i < ops.size(); i++) same = same_shape(G.ops[i], ops[i]);
+    if (same) {
+        for (size_t i = 0; same && i < ops.size(); i++) {
+            const StreamOp &a = ops[i], &b = G.ops[i];
+            if (a.kind == StreamOp::kKernel && a.args != b.args) {
+                void* p[32];
+                for (size_t j = 0; j < a.arg_off.size() && j < 32; j++) p[j] = (void*)(a.args.data() + a.arg_off[j]);
+                hipKernelNodeParams kp{};
+                kp.blockDim = a.block;
+                kp.gridDim = a.grid;
+                kp.func = const_cast<void*>(a.func);
+                kp.kernelParams = p;
+                kp.sharedMemBytes = a.lds;
+                same = hipGraphExecKernelNodeSetParams(G.exec, G.nodes[i], &kp) == hipSuccess;
+            } else if (a.kind == StreamOp::kCopy && (a.dst != b.dst || a.src != b.src || a.bytes != b.bytes)) {
+                same = hipGraphExecMemcpyNodeSetParams1D(G.exec, G.nodes[i], a.dst, a.src, a.bytes, a.ck) == hipSuccess;
+            }
+        }
+        if (same) {
+            G.ops = ops;
+            G.replays++;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    if (!same && !capture_ops(G, ops, st)) {
+        // (this device searches call by call from now on)
+        G.reset();
+        G.broken = true;
+        if (trace_on()) fprintf(stderr, "trace: search graph capture failed; direct launches\n");
+        issue_all(ops);
+        return 0;
+    }
+    check(hipGraphLaunch(G.exec, st), "graph launch");
+    return same ? 2u : 1u;
+}
+
 bool batch_pipelinable(size_t nqueries, size_t k) {
     return nqueries > 1 && k > 0 && k <= (size_t)kFilterMaxK && !cfg().no_filter;
 }
@@ -1278,11 +1412,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     // the counters are zeroed only when this search computes them)
     if (E > 0) {
         if (D.cnt_dirty) {
-            check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe + 16, D.stream), "memset");
+            check(op_set(D.d_cnt, 0, 16 * kMaxBatchPipe + 16, D.stream), "memset");
             D.gate_count = 0;
             D.cnt_dirty = false;
         } else if (want_counts) {
-            check(hipMemsetAsync(D.d_cnt, 0, 16 * kMaxBatchPipe, D.stream), "memset");
+            check(op_set(D.d_cnt, 0, 16 * kMaxBatchPipe, D.stream), "memset");
         }
     }
     const uint32_t gate0 = D.gate_count;
@@ -1315,6 +1449,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     // the rare-code merge (plan_view) needs the single-pass filter and no
     // counters (they decide from exact scores)
     const bool allow_merge = C.rare_merge && V == 1 && !ind && out.sparse && !want_counts && E > 0;
+    // option "graph": the usual search -- one query view, the device filter,
+    // no counters, the result copied back -- runs as a cached HIP graph
+    const bool use_graph = C.graph && !D.graph.broken && V == 1 && out.sparse && !ind && !want_counts &&
+                           !host_direct && !C.timeline && !C.side_tier && !allow_merge;
+    OpRecorder rec;
     if (allow_merge && D.alpha > 21) ensure_entry_masks(D);
     // every lane fits a view's overflow list (reference: no limit on the
     // sequences search_16.c:101-109 re-runs at 64 bits)
@@ -1501,7 +1640,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             // the reference skips the pair (no overflow)
             for (size_t e = 0; e < E; e++)
                 hs[e] = nw ? (int32_t)(Q + (int64_t)D.meta.len[e] * R) : 0;
-            if (want_counts) check(hipMemsetAsync(D.d_flags + v * E, 0, E, D.stream), "memset");
+            if (want_counts) check(op_set(D.d_flags + v * E, 0, E, D.stream), "memset");
             continue;
         }
         // which kernels, bounds and strip plan (plan_view); a fused batch
@@ -1701,14 +1840,20 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 memcpy(up_m + qm_off + 4 * i, &mi, 4);
             }
         if (!qpt.empty()) memcpy(up_q, qpt.data(), qpt.size() * 4);
-        if (!lean) check(hipEventRecord(D.ev[4], st), "event");
+        // a graph-eligible search records its stream operations from here to
+        // the result's copy and replays them as one HIP graph (run_ops)
+        if (use_graph) {
+            rec.ops.clear();
+            op_recorder() = &rec;
+        }
+        if (!lean) check(op_record(D.ev[4], st, true), "event");
         if (!qpt.empty())
-            check(hipMemcpyAsync(dqpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
+            check(op_copy(dqpt, up_q, qpt.size() * 4, hipMemcpyHostToDevice, st), "H2D qpt");
         if (C.upload_kernel)
             check(launch_upload(dup, up_m, (blk_bytes + 3) & ~(size_t)3, st), "upload kernel");
         else
-            check(hipMemcpyAsync(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
-        if (piped) check(hipEventRecord(D.ev[5], st), "event");   // staging buffer free again
+            check(op_copy(dup, up_m, blk_bytes, hipMemcpyHostToDevice, st), "H2D uploads");
+        if (piped) check(op_record(D.ev[5], st), "event");   // staging buffer free again
         // overflow list of this view: the whole list, or in a multi-view
         // search its own slice (all views stay on the device until the end)
         uint32_t* ovf = D.d_ovf + (piped ? v * (ovf_capv + 1) : 0);
@@ -1804,7 +1949,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 ra.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)ra.blocks * kLongWaves * ra.stride;
                 if (D.rscratch_cap < need) {
-                    if (piped && v > 0) check(hipStreamSynchronize(D.stream), "sync");
+                    if (piped && v > 0) sync_point(D.stream, "sync");
                     dfree(D.d_rscratch);
                     check(hipMalloc((void**)&D.d_rscratch, need * 8), "re-score scratch");
                     D.rscratch_cap = need;
@@ -1828,11 +1973,19 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 check(hipMalloc((void**)&D.d_timeline, rows * sizeof(uint4)), "timeline");
                 D.timeline_cap = rows;
             }
-            check(hipMemsetAsync(D.d_timeline, 0, rows * sizeof(uint4), st), "memset");
+            check(op_set(D.d_timeline, 0, rows * sizeof(uint4), st), "memset");
             D.timeline_rows = rows;
             tl = D.d_timeline;
         }
-        check(hipEventRecord(ev_k0, st), "event");
+        check(op_record(ev_k0, st, true), "event");
+        // the long-entry streams fork from here: in a recorded search through
+        // an event of its own (ev_k0 becomes a timing node of the graph,
+        // which carries no dependency), otherwise through ev_k0 itself
+        hipEvent_t fork_ev = ev_k0;
+        if (op_recorder()) {
+            fork_ev = D.ev_fork;
+            check(op_record(fork_ev, st), "event");
+        }
         std::vector<std::function<void()>> long_launch;   // the long-entry kernels' launches
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
@@ -1888,9 +2041,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             if (need_hmm) {
                 if (D.hmm_cap < (size_t)long_groups * 64) {
-                    check(hipStreamSynchronize(D.stream_long), "sync");
-                    check(hipStreamSynchronize(D.stream_long1), "sync");
-                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                    sync_point(D.stream_long, "sync");
+                    sync_point(D.stream_long1, "sync");
+                    if (piped && v > 0) sync_point(st, "sync");
                     dfree(D.d_hmm);
                     check(hipMalloc((void**)&D.d_hmm, (size_t)long_groups * 64 * sizeof(int2)), "long-entry extremes");
                     D.hmm_cap = (size_t)long_groups * 64;
@@ -1907,8 +2060,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 la.stride = D.group_ncols[0] + 16;
                 const size_t need = (size_t)long_groups * 64 * la.stride;
                 if (D.lscratch_cap < need) {
-                    check(hipStreamSynchronize(D.stream_long), "sync");
-                    check(hipStreamSynchronize(D.stream_long1), "sync");
+                    sync_point(D.stream_long, "sync");
+                    sync_point(D.stream_long1, "sync");
                     dfree(D.d_lscratch);
                     check(hipMalloc((void**)&D.d_lscratch, need * 8), "long-entry scratch");
                     D.lscratch_cap = need;
@@ -1928,9 +2081,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 gate_total += la.nseq;                         // one workgroup per entry
                 D.gate_count += la.nseq;
                 long_launch.push_back([=, &D]() {
-                    check(hipStreamWaitEvent(D.stream_long, ev_k0, 0), "event wait");
+                    check(op_wait(D.stream_long, fork_ev), "event wait");
                     check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
-                    check(hipEventRecord(D.ev[7], D.stream_long), "event");
+                    check(op_record(D.ev[7], D.stream_long), "event");
                 });
             }
             if (long4 < long_groups) {
@@ -1945,10 +2098,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
                 }
                 long_launch.push_back([=, &D]() {
-                    check(hipStreamWaitEvent(D.stream_long1, ev_k0, 0), "event wait");
+                    check(op_wait(D.stream_long1, fork_ev), "event wait");
                     if (rl16 > 0) check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
                     else check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
-                    check(hipEventRecord(D.ev[6], D.stream_long1), "event");
+                    check(op_record(D.ev[6], D.stream_long1), "event");
                 });
             }
             if (v == 0) {
@@ -2009,7 +2162,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {
-            check(hipMemsetAsync(ovf, 0, 4, st), "memset");
+            check(op_set(ovf, 0, 4, st), "memset");
         }
         for (auto& f : long_launch) f();
 
@@ -2058,7 +2211,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 if (parts > 2 && !D.d_rowbuf3 && D.ngroups > long_groups) {
                     // the third part's row buffer (4 B per residue slot); without
                     // the memory for it the search runs two parts
-                    if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                    if (piped && v > 0) sync_point(st, "sync");
                     if (hipMalloc((void**)&D.d_rowbuf3, (size_t)D.nblocks * 4096) != hipSuccess) {
                         (void)hipGetLastError();
                         D.d_rowbuf3 = nullptr;
@@ -2070,11 +2223,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     const uint32_t ps = (T + parts - 1) / parts;
                     parts = (T + ps - 1) / ps;
                     if (D.part_cap < quads * nqf || D.smax_cap < (size_t)D.ngroups * 64 * nqf) {
-                        if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                        if (piped && v > 0) sync_point(st, "sync");
                         if (D.part_cap < quads * nqf) {
                             dfree(D.d_part);
                             check(hipMalloc((void**)&D.d_part, (size_t)quads * nqf * 4), "strip parts");
-                            check(hipMemsetAsync(D.d_part, 0, (size_t)quads * nqf * 4, st), "memset");
+                            check(op_set(D.d_part, 0, (size_t)quads * nqf * 4, st), "memset");
                             D.part_cap = quads * nqf;
                         }
                         if (D.smax_cap < (size_t)D.ngroups * 64 * nqf) {
@@ -2113,7 +2266,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                         b.rowbuf2 = (uint4*)(D.d_rowbuf_q + nqf * (size_t)D.nblocks * 4096);
                     } else {
                         if (!D.d_rowbuf2) {
-                            if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                            if (piped && v > 0) sync_point(st, "sync");
                             check(hipMalloc((void**)&D.d_rowbuf2, (size_t)D.nblocks * 4096), "second row buffer");
                         }
                         b.rowbuf2 = D.d_rowbuf2;
@@ -2169,7 +2322,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             // a fused batch's DP time runs from this one launch (not from view
             // 0's start: the host prepared the other views in between)
-            if (fused && v + 1 == V) check(hipEventRecord(D.vev[2 * V], st), "event");
+            if (fused && v + 1 == V) check(op_record(D.vev[2 * V], st, true), "event");
             if (!fused || v + 1 == V)
                 check(launch_pair(b, pnp, tail_np, nw, (size_t)pair_lds_rows(A) * (lnp + 4) * 4, st), "pair kernel launch");
         } else {
@@ -2179,14 +2332,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // overflow flags, its filter pass (a fused batch defers it until the
         // one pair launch that covers every view)
         auto post = [=, &D, &kernel_bytes, &counted]() {
-            if (long4 > 0) check(hipStreamWaitEvent(st, D.ev[7], 0), "event wait");
-            if (long4 < long_groups) check(hipStreamWaitEvent(st, D.ev[6], 0), "event wait");
-            check(hipEventRecord(ev_k1, st), "event");
+            if (long4 > 0) check(op_wait(st, D.ev[7]), "event wait");
+            if (long4 < long_groups) check(op_wait(st, D.ev[6]), "event wait");
+            check(op_record(ev_k1, st, true), "event");
             if (side_tier) {
                 // (header cleared by the tables kernel; no counters)
-                check(hipStreamWaitEvent(D.stream_long1, ev_k1, 0), "event wait");
+                check(op_wait(D.stream_long1, ev_k1), "event wait");
                 check(launch_long(ra, 1, rl32, nw, D.stream_long1), "int32 re-score launch");
-                check(hipEventRecord(D.ev[8], D.stream_long1), "event");
+                check(op_record(D.ev[8], D.stream_long1), "event");
             } else if (defer_tier) {
                 // (after the result's copy, if the header reports overflowed lanes)
             } else if (rl32 > 0) {
@@ -2262,7 +2415,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     fa.rthreads = (uint32_t)std::max<size_t>(64, std::min<size_t>(1024, (64ull << 20) / (8ull * fa.rstride)) / 64 * 64);
                     const size_t need = (size_t)fa.rthreads * 2 * fa.rstride;
                     if (D.frwork_cap < need) {
-                        if (piped && v > 0) check(hipStreamSynchronize(st), "sync");
+                        if (piped && v > 0) sync_point(st, "sync");
                         dfree(D.d_frwork);
                         check(hipMalloc((void**)&D.d_frwork, need * 4), "row-major replay scratch");
                         D.frwork_cap = need;
@@ -2282,7 +2435,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     check(launch_count(ca, st), "overflow count launch");
                 }
                 if (v + 1 == V) {
-                    check(hipMemcpyAsync(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st), "D2H counters");
+                    check(op_copy(D.h_cnt, D.d_cnt, 16 * (ind ? V : 1), hipMemcpyDeviceToHost, st), "D2H counters");
                     counted = true;
                 }
             }
@@ -2307,7 +2460,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.status = gate + 2;
                 f.cand = (uint2*)(reg + kFilterHeader);
                 check(launch_filter(f, st), "filter launch");
-                check(hipMemcpyAsync((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
+                check(op_copy((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
                                      hipMemcpyDeviceToHost, st), "D2H candidates");
             }
         };
@@ -2342,12 +2495,12 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             f.q_counters = dreg / 4;
             check(launch_filter(f, st), "filter launch");
             for (size_t vv = 0; vv < V; vv++)
-                check(hipMemcpyAsync((uint8_t*)D.h_fbuf + vv * hreg, (uint8_t*)D.d_fbuf + vv * dreg,
+                check(op_copy((uint8_t*)D.h_fbuf + vv * hreg, (uint8_t*)D.d_fbuf + vv * dreg,
                                      kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E), hipMemcpyDeviceToHost, st),
                       "D2H candidates");
         }
         if (piped && v + 1 < V) continue;
-        if (!lean) check(hipEventRecord(D.ev[2], st), "event");
+        if (!lean) check(op_record(D.ev[2], st, true), "event");
         if (ind) {
             // (filters already enqueued per query)
         } else if (out.sparse) {
@@ -2388,7 +2541,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             check(launch_filter(f, st), "filter launch");
             // (the stream's end, and so the host's wake-up, covers the tier)
-            if (side_tier) check(hipStreamWaitEvent(st, D.ev[8], 0), "event wait");
+            if (side_tier) check(op_wait(st, D.ev[8]), "event wait");
             if (merge) {
                 // the forwarded merged-code entries, exactly: the int32 tier
                 // over their lanes (count: the filter header's word 1) on the
@@ -2413,7 +2566,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     xa.stride = D.group_ncols[0] + 16;
                     const size_t need = (size_t)xa.blocks * kLongWaves * xa.stride;
                     if (D.rscratch_cap < need) {
-                        check(hipStreamSynchronize(st), "sync");
+                        sync_point(st, "sync");
                         dfree(D.d_rscratch);
                         check(hipMalloc((void**)&D.d_rscratch, need * 8), "re-score scratch");
                         D.rscratch_cap = need;
@@ -2422,8 +2575,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 }
                 check(launch_long(xa, 1, vp.merge_rl, nw, st), "exact re-score launch");
                 const size_t nx = std::min(kExactPinned, D.exact_cap);
-                check(hipMemcpyAsync(D.h_exact, D.d_exact, nx * 4, hipMemcpyDeviceToHost, st), "D2H exact lanes");
-                check(hipMemcpyAsync(D.h_exact + kExactPinned * 4, D.d_exact + xcap_al, nx * 8, hipMemcpyDeviceToHost, st),
+                check(op_copy(D.h_exact, D.d_exact, nx * 4, hipMemcpyDeviceToHost, st), "D2H exact lanes");
+                check(op_copy(D.h_exact + kExactPinned * 4, D.d_exact + xcap_al, nx * 8, hipMemcpyDeviceToHost, st),
                       "D2H exact scores");
             }
             if (!host_direct) {
@@ -2434,22 +2587,27 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const size_t first = std::min<size_t>(std::min<size_t>(D.h_cand_cap, f.n),
                                                       std::max<size_t>(256, 2 * (size_t)D.cand_hint + 64));
                 D.cand_first = first;
-                check(hipMemcpyAsync(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
+                check(op_copy(D.h_fbuf, D.d_fbuf, kFilterHeader * 4 + 8 * first, hipMemcpyDeviceToHost, st),
                       "D2H candidates");
             }
         } else {
-            check(hipMemcpyAsync(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
+            check(op_copy(hs, D.d_scores, E * 4, hipMemcpyDeviceToHost, st), "D2H scores");
             // (the first kOvfPinned entries; d_ovf holds ovf_capv + 1 dwords)
             const size_t pre = std::min(kOvfPinned, ovf_capv);
-            check(hipMemcpyAsync(D.h_ovf, D.d_ovf, 4 * (pre + 1), hipMemcpyDeviceToHost, st), "D2H overflow");
-            check(hipMemcpyAsync(D.h_wide, D.d_wide, 8 * pre, hipMemcpyDeviceToHost, st), "D2H wide");
+            check(op_copy(D.h_ovf, D.d_ovf, 4 * (pre + 1), hipMemcpyDeviceToHost, st), "D2H overflow");
+            check(op_copy(D.h_wide, D.d_wide, 8 * pre, hipMemcpyDeviceToHost, st), "D2H wide");
         }
         // the strip-part wait status: the filter passes copy it into their
         // candidate headers (word 2); only a search without them reads it back
         uint32_t* const h_perr = (uint32_t*)(D.h_cnt + 2 * kMaxBatchPipe) + 2;
         const bool perr_in_header = ind || out.sparse;
         if (parts_used && !perr_in_header)
-            check(hipMemcpyAsync(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
+            check(op_copy(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
+        out.graph = 0;
+        if (op_recorder()) {
+            op_recorder() = nullptr;
+            out.graph = run_ops(D, rec, st);
+        }
         const double t_sync0 = now_ms();
         // filter_host 3: the filter's own stores, made visible by the end of
         // its dispatch -- an ordinary synchronisation, no copy, no spin

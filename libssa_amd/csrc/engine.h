@@ -29,6 +29,19 @@ struct DeviceDB {
     int symtype = -1, strands = -1, dgencode = -1;
     hipStream_t stream = nullptr;
     hipEvent_t ev[9] = {};                // [8]: the int32 tier's end when it runs beside the filter
+    hipEvent_t ev_fork = nullptr;         // a recorded search's fork to the long-entry streams
+    // the last graph-eligible search's stream operations as an instantiated
+    // HIP graph (engine.cpp run_ops): replayed while the next search issues
+    // the same operations, its changed arguments set on their nodes
+    struct SearchGraph {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<StreamOp> ops;
+        std::vector<hipGraphNode_t> nodes;   // per op: its node (kernels, copies, sets)
+        bool broken = false;                 // capture or instantiation failed once: direct from then on
+        uint64_t captures = 0, replays = 0;
+        void reset();
+    } graph;
     EntryMeta meta;
     uint32_t ngroups = 0;
     uint64_t nblocks = 0;                 // 1 KiB residue blocks
@@ -217,6 +230,7 @@ struct SearchScores {
     uint32_t part_retries = 0;           // 1: a strip-part wait timed out, the search ran again without parts
     uint32_t rare_merged = 0;            // compact codes scored through one upper-bound class (0: none)
     uint32_t rare_rescored = 0;          // forwarded merged-code entries re-scored exactly
+    uint32_t graph = 0;                  // 0 direct, 1 captured into a new graph, 2 replayed (stats graph)
     int64_t get(size_t v, size_t e) const {
         const int32_t x = s32[v * entries + e];
         if (x != INT32_MIN) return x;

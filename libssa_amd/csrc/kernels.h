@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "launch.h"
+
 namespace ssa {
 
 constexpr int kWaves = 4;          // waves (= 64-sequence groups) per workgroup

@@ -830,17 +830,17 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
     const uint32_t nq = a.nq > 1 ? a.nq : 1u;
-    hipLaunchKernelGGL(filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
     if (g_prefix_regs && a.nblocks <= (uint32_t)(kPrefixWaves * kPrefixRegs)) {
-        if (a.k <= 16) hipLaunchKernelGGL(filter_prefix_r<16>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
-        else if (a.k <= 32) hipLaunchKernelGGL(filter_prefix_r<32>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
-        else hipLaunchKernelGGL(filter_prefix_r<64>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        if (a.k <= 16) (void)ssa_launch((const void*)&filter_prefix_r<16>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        else if (a.k <= 32) (void)ssa_launch((const void*)&filter_prefix_r<32>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        else (void)ssa_launch((const void*)&filter_prefix_r<64>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
     } else {
-        hipLaunchKernelGGL(filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
+        (void)ssa_launch((const void*)&filter_prefix, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);
     }
     if (a.host_out && (nq > 1 || !a.done)) return hipErrorInvalidValue;
     const uint32_t sel = std::max<uint32_t>((a.n + 256 * kSelectPer - 1) / (256 * kSelectPer), (a.nviews + 255) / 256);
-    hipLaunchKernelGGL(filter_select, dim3(sel, nq), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&filter_select, dim3(sel, nq), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -909,7 +909,7 @@ hipError_t launch_upload(void* dst, const void* src, size_t bytes, hipStream_t s
     if ((bytes & 3) || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3)) return hipErrorInvalidValue;
     const uint32_t n4 = (uint32_t)(bytes / 4);
     const uint32_t blocks = std::min<uint32_t>((n4 + 255) / 256, 64);
-    hipLaunchKernelGGL(upload_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)dst, (const uint32_t*)src, n4);
+    (void)ssa_launch((const void*)&upload_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)dst, (const uint32_t*)src, n4);
     return hipGetLastError();
 }
 
@@ -918,17 +918,17 @@ hipError_t launch_pair_tables(const TableArgs& a, hipStream_t st) {
     const size_t total = (size_t)prow * prow * ((size_t)a.np * a.nmain + pair_tail_pitch(a.npt));
     if (total == 0) {
         if (a.zero_hdr) {
-            const hipError_t e = hipMemsetAsync(a.zero_hdr, 0, 4 * a.nzero_hdr, st);
+            const hipError_t e = op_set(a.zero_hdr, 0, 4 * a.nzero_hdr, st);
             if (e != hipSuccess) return e;
         }
         if (a.zero_ticket) {
-            const hipError_t e = hipMemsetAsync(a.zero_ticket, 0, 4, st);
+            const hipError_t e = op_set(a.zero_ticket, 0, 4, st);
             if (e != hipSuccess) return e;
         }
-        return a.zero ? hipMemsetAsync(a.zero, 0, 4, st) : hipSuccess;
+        return a.zero ? op_set(a.zero, 0, 4, st) : hipSuccess;
     }
     const uint32_t blocks = (uint32_t)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(pair_tables_kernel, dim3(blocks), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&pair_tables_kernel, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -954,7 +954,7 @@ __global__ void __launch_bounds__(256) recode_kernel(const RecodeArgs a) {
 hipError_t launch_recode(const RecodeArgs& a, hipStream_t st) {
     if (a.n16 == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)std::min<size_t>((a.n16 + 255) / 256, 8192);
-    hipLaunchKernelGGL(recode_kernel, dim3(blocks), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&recode_kernel, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1011,13 +1011,13 @@ __global__ void __launch_bounds__(256) entry_mask_kernel(const EntryMaskArgs a) 
 
 hipError_t launch_entry_mask(const EntryMaskArgs& a, hipStream_t st) {
     if (a.ngroups == 0) return hipSuccess;
-    hipLaunchKernelGGL(entry_mask_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&entry_mask_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
 hipError_t launch_pair_addr(const PairAddrArgs& a, hipStream_t st) {
     if (a.ngroups == 0) return hipSuccess;
-    hipLaunchKernelGGL(pair_addr_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
+    (void)ssa_launch((const void*)&pair_addr_kernel, dim3((a.ngroups + 3) / 4), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1449,7 +1449,7 @@ static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
     if (a.list && (W != 1 || a.blocks == 0 || a.hmm || a.timeline || a.gate)) return hipErrorInvalidValue;
     LongArgs b = a;
     if (!a.list) b.blocks = (a.nseq + EPW - 1) / EPW;
-    hipLaunchKernelGGL((long_kernel<W, RL, NW, TRK>), dim3(b.blocks), dim3(64 * kLongWaves), bytes, st, b);
+    (void)ssa_launch((const void*)&long_kernel<W, RL, NW, TRK>, dim3(b.blocks), dim3(64 * kLongWaves), bytes, st, b);
     return hipGetLastError();
 }
 
@@ -1868,7 +1868,7 @@ static hipError_t launch_long16_k(const LongArgs& a, hipStream_t st) {
     // profiles/r05/ab/l16w8_sprot -- a finished workgroup's hole waits for
     // its longest entry, and more prio-3 waves starve the pair waves beside them)
     const uint32_t blocks = (a.nseq + kLongWaves - 1) / kLongWaves;
-    hipLaunchKernelGGL((long16_kernel<RL>), dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
+    (void)ssa_launch((const void*)&long16_kernel<RL>, dim3(blocks), dim3(64 * kLongWaves), bytes, st, a);
     return hipGetLastError();
 }
 
@@ -1891,7 +1891,7 @@ template <int NP, bool NW>
 static hipError_t launch_np(const StripArgs& a, hipStream_t st) {
     const uint32_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((strip16_kernel<NP, NW>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    (void)ssa_launch((const void*)&strip16_kernel<NP, NW>, dim3(blocks), dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1904,9 +1904,9 @@ hipError_t launch_strip16(const StripArgs& a, int np, bool nw, hipStream_t st) {
 hipError_t launch_sw_f16(const StripArgs& a, int np, hipStream_t st) {
     const uint32_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     if (blocks == 0) return hipSuccess;
-    if (np == 8) hipLaunchKernelGGL((strip_f16m_kernel<8>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
-    else if (np == 32) hipLaunchKernelGGL((strip_f16m_kernel<32>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
-    else hipLaunchKernelGGL((strip_f16m_kernel<16>), dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    if (np == 8) (void)ssa_launch((const void*)&strip_f16m_kernel<8>, dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    else if (np == 32) (void)ssa_launch((const void*)&strip_f16m_kernel<32>, dim3(blocks), dim3(64 * kWaves), 0, st, a);
+    else (void)ssa_launch((const void*)&strip_f16m_kernel<16>, dim3(blocks), dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1924,7 +1924,7 @@ hipError_t launch_pair(const StripArgs& a, int np, int npt, bool nw, size_t lds_
 
 hipError_t launch_wide(const WideArgs& a, uint32_t threads, hipStream_t st) {
     const uint32_t blocks = (threads + 63) / 64;
-    hipLaunchKernelGGL(wide_kernel, dim3(blocks), dim3(64), 0, st, a);
+    (void)ssa_launch((const void*)&wide_kernel, dim3(blocks), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

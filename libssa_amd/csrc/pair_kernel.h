@@ -601,7 +601,7 @@ static hipError_t launch_pair_t(const StripArgs& a, size_t lds_bytes, hipStream_
     if (a.nq > (uint32_t)kMaxFuse) return hipErrorInvalidValue;
     const uint32_t units = a.nparts > 1 ? quads + (a.nparts - 1) * (a.split_q1 - a.split_q0) : quads;
     const uint32_t blocks = units * std::max(a.nq, 1u);
-    hipLaunchKernelGGL((pair_kernel<NP, NW, NPT>), dim3(blocks), dim3(64 * W), lds_bytes, st, a);
+    (void)ssa_launch((const void*)&pair_kernel<NP, NW, NPT>, dim3(blocks), dim3(64 * W), lds_bytes, st, a);
     return hipGetLastError();
 }
 

@@ -99,9 +99,12 @@ def test_native_merge_logs_equals_single_process(cuts, k):
 @pytest.mark.gpu
 def test_native_rccl_gather_world1(tmp_path):
     """ssa_amd_dist_init + ssa_amd_gather_logs over RCCL with one rank (the
-    one-GPU box; the driver's 8-GPU run exercises N > 1): the fixed-slot
-    all-gather and the exact-size ncclGather round (a log longer than the
-    512-row slot) both return the replayed top-k."""
+    one-GPU box; the driver's 8-GPU run exercises N > 1): the ncclGather of
+    fixed 513-row slots, for a log within the slot and one longer than it
+    (rank 0's own rows beyond the slot are read from memory; with one rank no
+    point-to-point remainder is sent -- that path runs over RCCL only at
+    N > 1 and in-process in test_native_gather_fake_world), returns the
+    replayed top-k."""
     import libssa_amd as S
     S.load()
     S.set_device(0)
@@ -428,6 +431,7 @@ class _FakeLib:
     def stats(self):
         n = len(self.devices)
         return {"total_searches": self.searches, "total_kernel_ms": float(n) * self.searches, "slots": n,
+                "search_ms": 0.5 + n,
                 "slot_device": list(self.devices), "slot_kernel_ms": [1.0 + s for s in range(n)],
                 "slot_search_ms": [1.25 + s for s in range(n)]}
 
@@ -474,6 +478,7 @@ def test_bench_drop_in_record_on_gloo_rehearsal(tmp_path, world):
     assert d["slot_search_ms"] == [1.25 + s for s in range(world)]
     sp = d["step_split_ms"]
     assert sp["slowest_slot"] == world - 1 and sp["slot_kernel"] == world and sp["slot_host"] == 0.25
+    assert sp["search"] == 0.5 + world and sp["merge_and_rest"] == 0.25
     assert abs(sp["step"] - d["ms_per_step"]) < 1e-3 and d["value"] > 0
     assert d["top_hit"] == [100, 0] and "topk_vs_reference" not in d      # (a 3000-ID slice: no fixture)
     assert r0["searches"] == 4 + 2                                            # warm-up, 4 timed, the result

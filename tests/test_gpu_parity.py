@@ -856,6 +856,60 @@ def test_filter_host_with_side_tier_overflow():
         S.free_sequence(qq)
 
 
+def test_search_graph_replays_exactly():
+    """Option graph (default 1): the usual search's stream operations --
+    upload, tables, long-entry kernels on their own streams, the pair kernel
+    with strip parts, the filter, the result's copy -- are captured once per
+    launch plan into a HIP graph and replayed with the changed arguments (gate
+    target, strip-part epoch, copy length) set on their nodes.  Results equal
+    the call-by-call path and the oracle over alternating plans (query
+    lengths, SW/NW, k), repeated queries replay the cached graph (stats graph
+    2), a new plan is captured (1), and kernel_ms, read from the graph's own
+    event nodes, stays that of the direct path."""
+    rng = np.random.default_rng(41)
+    codes, off = syn.protein_db(20000, 42, lo=1, hi=1200)
+    # a few long entries: the long-entry streams join the graph
+    lens = np.diff(off).astype(np.int64)
+    seqs = [codes[int(off[i]):int(off[i + 1])] for i in range(len(lens))]
+    for i in range(0, 300, 3):
+        seqs[i] = rng.choice(syn.AA_CODES, int(rng.integers(3000, 6000))).astype(np.uint8)
+    db, doff = po.pack_db(seqs)
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    ids = np.arange(len(seqs), dtype=np.uint64)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    with tempfile.TemporaryDirectory() as tmp:
+        S.init_db(_write_db(tmp, db, doff))
+        qs = {n: syn.protein_query(n, 900 + n) for n in (60, 250, 400)}
+        qq = {n: S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q)) for n, q in qs.items()}
+        exp = {(n, a): po.scores(a, q, db, doff, M, -11, -1) for n, q in qs.items() for a in (S.SW, S.NW)}
+        order = [(400, S.SW, 10)] * 3 + [(60, S.SW, 10), (400, S.SW, 10), (250, S.NW, 64), (250, S.NW, 64),
+                                         (400, S.SW, 1), (400, S.SW, 64), (60, S.NW, 10), (60, S.NW, 10)]
+        try:
+            S.set_option("long_groups", 2)
+            got = {}
+            for g in (1, 0):
+                S.set_option("graph", g)
+                got[g] = []
+                for n, a, k in order:
+                    fn = S.sw_align if a == S.SW else S.nw_align
+                    hits = [(h["score"], h["id"]) for h in fn(qq[n], k, 16)]
+                    st = S.stats()
+                    got[g].append((hits, st["graph"], st["kernel_ms"]))
+                    assert hits == po.topk(exp[(n, a)], ids, k), (g, n, a, k)
+            assert [x[0] for x in got[1]] == [x[0] for x in got[0]]
+            modes = [x[1] for x in got[1]]
+            assert all(m == 0 for _, m, _ in got[0]), [x[1] for x in got[0]]
+            assert modes[0] in (1, 2) and modes[1] == 2 and modes[2] == 2, modes
+            assert modes[4] in (1, 2) and modes[6] == 2 and modes[10] == 2, modes
+            for (h1, m1, k1), (h0, m0, k0) in zip(got[1], got[0]):
+                assert 0 < k1 and 0.5 * k0 < k1 < 2.0 * k0 + 0.05, (k1, k0)
+        finally:
+            S.set_option("graph", 1)
+            S.set_option("long_groups", -1)
+        for q in qq.values():
+            S.free_sequence(q)
+
+
 def test_shard_logs_replay_to_global_result():
     """The insertion logs of consecutive ID shards, concatenated in shard
     order and replayed, equal the single-DB top-k including tie IDs."""
