@@ -100,6 +100,7 @@ def parse():
     p.add_argument("--no-drop-in", action="store_true",
                    help="N>1: skip the drop_in record (the north-star DB through sw_align on all N devices of "
                         "rank 0's process, after the multi-process records)")
+    p.add_argument("--drop-in-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--drop-in-seqs", type=int, default=None,
                    help="drop_in record: the first S IDs of the north-star DB instead of all 10 M")
     p.add_argument("--long-tail", type=int, default=None,
@@ -715,28 +716,19 @@ def north_star(S, args, job):
     return rec
 
 
-def drop_in(S, args, job, torch_sync=None):
-    """N > 1, after the multi-process records: the drop-in path -- an
-    UNCHANGED libssa caller on all N GPUs of the node from ONE process, as
-    SSA_AMD_DEVICES routes it (include/libssa_amd.h: the library's persistent
-    per-device slot threads inside sw_align, the DB split into chunk-aligned
-    residue-balanced record ranges, the slot logs merged on the host; the
-    reference's own default is every core of the machine,
-    src/util/thread_pool.c:39-47, its heaps merged in thread order,
-    src/algo/manager.c:141-145).  Ranks != 0 release their device DBs
-    (ssa_exit) and wait at a barrier; rank 0 opens the north-star DB (the
-    fixed 10 M sequences; --drop-in-seqs: its first S IDs), selects one device
-    slot per rank (ssa_amd_set_devices -- a rehearsal's ranks share GPUs, so
-    do its slots) and times free_alignment(sw_align(...)) exactly as the N = 1
-    headline.  Returns rank 0's record (None elsewhere)."""
-    if job.rank != 0:
-        S.ssa_exit()
-        job.dist.barrier()
-        return None
-    S.ssa_exit()
+def drop_in_measure(S, args, torch_sync=None):
+    """The drop_in record's measurement, run in a process of its own
+    (bench.py --drop-in-child, started by drop_in below with SSA_AMD_DEVICES
+    set): an UNCHANGED libssa caller -- no ssa_amd_set_device(s) call -- opens
+    the north-star DB (the fixed 10 M sequences; --drop-in-seqs: its first S
+    IDs) and the library, reading SSA_AMD_DEVICES at init_db, searches it on
+    every listed device (include/libssa_amd.h: one persistent host thread per
+    device slot inside sw_align, the DB cut into chunk-aligned residue-balanced
+    record ranges, the slot logs merged on the host; the reference's own
+    default is every core of the machine, src/util/thread_pool.c:39-47, its
+    heaps merged in thread order, src/algo/manager.c:141-145).
+    free_alignment(sw_align(...)) is timed exactly as the N = 1 headline."""
     w = workload(args, "north_star", overrides=False)
-    n_gpus = max(1, args.n_gpus)
-    devices = [r % n_gpus for r in range(job.world)]
     from libssa_amd import synthetic as syn
     t0 = time.time()
     configure(S, w)
@@ -748,8 +740,8 @@ def drop_in(S, args, job, torch_sync=None):
     syn.write_fasta(path, codes, off)
     residues, seqs = int(off[-1]), len(off) - 1
     del codes, off
-    assert S.set_devices(devices) == 0, devices
     S.init_db(path)
+    devices = list(S.get_devices())
     S.set_id_offset(0)
     S.prepare_db()
     os.remove(path)
@@ -772,9 +764,6 @@ def drop_in(S, args, job, torch_sync=None):
     res = S.align_scores(qq, k, w.width, S.SW)             # untimed: the result and its per-slot split
     last = S.stats()
     S.free_sequence(qq)
-    S.ssa_exit()
-    S.set_devices([])
-    S.set_device(job.dev_index)
     cells = float(residues) * len(q)
     step_ms = elapsed / steps * 1e3
     n = max(1, st1["total_searches"] - st0["total_searches"])
@@ -782,7 +771,8 @@ def drop_in(S, args, job, torch_sync=None):
     slow = int(np.argmax(ssm)) if ssm else 0
     rec = {
         "workload": "SW int16 BLOSUM62 gaps -11/-1, 400-residue query (seed 7) vs the north-star DB, one process, "
-                    "sw_align on every slot (an unchanged libssa caller under SSA_AMD_DEVICES)",
+                    "an unchanged sw_align caller on every device SSA_AMD_DEVICES lists",
+        "ssa_amd_devices": os.environ.get("SSA_AMD_DEVICES"),
         "devices": devices, "slots": int(last["slots"]), "bit_width": 16, "steps": steps, "warmup": 1,
         "db_seqs": seqs, "db_residues": residues, "cells_per_step": cells,
         "ms_per_step": round(step_ms, 3), "value": round(cells / (elapsed / steps) / 1e9, 2), "unit": "GCUPS",
@@ -803,6 +793,52 @@ def drop_in(S, args, job, torch_sync=None):
     m = fixture_match(w, sh, res, k, 1)
     if m is not None:
         rec["topk_vs_reference"] = m
+    return rec
+
+
+def _run_child(cmd, env, timeout=900):
+    """Runs the drop_in child; its last JSON line, or what went wrong."""
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"drop_in child exceeded {timeout} s"}
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"drop_in child exited with status {r.returncode}", "stderr_tail": r.stderr[-1500:]}
+    return json.loads(lines[-1])
+
+
+def drop_in(S, args, job, runner=None):
+    """N > 1, after the multi-process records: the drop-in path, measured.
+    Ranks != 0 release their device DBs (ssa_exit) and wait at a barrier;
+    rank 0 releases its own and starts `bench.py --drop-in-child` with
+    SSA_AMD_DEVICES listing one device slot per rank (a rehearsal's ranks
+    share GPUs, so do its slots) -- a process of its own, so that whatever the
+    single-process multi-GPU path does cannot take the multi-process line
+    down with it (its failure becomes the record's "error").  Returns rank
+    0's record (None elsewhere)."""
+    if job.rank != 0:
+        S.ssa_exit()
+        job.dist.barrier()
+        return None
+    S.ssa_exit()
+    n_gpus = max(1, args.n_gpus)
+    devices = [r % n_gpus for r in range(job.world)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    env["SSA_AMD_DEVICES"] = ",".join(map(str, devices))
+    cmd = [sys.executable, os.path.abspath(__file__), "--drop-in-child", "--k", str(args.k), "--steps", str(args.steps)]
+    if args.north_star_steps is not None:
+        cmd += ["--north-star-steps", str(args.north_star_steps)]
+    if args.drop_in_seqs is not None:
+        cmd += ["--drop-in-seqs", str(args.drop_in_seqs)]
+    for o in getattr(args, "option", []):
+        cmd += ["--option", o]
+    t0 = time.time()
+    rec = (runner or _run_child)(cmd, env)
+    rec["child_wall_s"] = round(time.time() - t0, 1)
+    rec["devices_requested"] = devices
     job.dist.barrier()
     return rec
 
@@ -815,6 +851,18 @@ def main():
     if args.launch_selftest:
         if "WORLD_SIZE" in os.environ:
             launch_selftest(args)
+        return
+    if args.drop_in_child:
+        # (drop_in's child: no torch, no process group; the library reads
+        # SSA_AMD_DEVICES at its first init_db -- this process never selects
+        # a device itself)
+        import libssa_amd as S
+        S.load()
+        S.set_output_mode(S.OUTPUT_ERROR)
+        for o in args.option:
+            k, v = o.split("=")
+            S.set_option(k, int(v))
+        print(json.dumps(drop_in_measure(S, args)), flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -878,9 +926,8 @@ def main():
     # --- the drop-in record (N > 1: one process on all N devices)
     di = None
     if world > 1 and not args.no_drop_in:
-        import torch
-        di = drop_in(S, args, job, torch.cuda.synchronize if dev == "cuda" else None)
-        if di is not None and ns is not None and ns.get("value"):
+        di = drop_in(S, args, job)
+        if di is not None and ns is not None and ns.get("value") and di.get("value"):
             di["vs_multi_process"] = round(di["value"] / ns["value"], 4)
     if rank != 0:
         dist.destroy_process_group()

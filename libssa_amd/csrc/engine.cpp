@@ -52,6 +52,7 @@ void DeviceDB::SearchGraph::reset() {
     g = nullptr;
     ops.clear();
     nodes.clear();
+    used = 0;
 }
 
 void DeviceDB::release() {
@@ -1278,6 +1279,7 @@ static void issue_all(const std::vector<StreamOp>& ops) {
 // it stands and the rest of the search runs call by call.
 static void sync_point(hipStream_t s, const char* what) {
     if (OpRecorder* r = op_recorder()) {
+        if (trace_on()) fprintf(stderr, "trace: search graph: sync point (%s) after %zu ops\n", what, r->ops.size());
         op_recorder() = nullptr;
         issue_all(r->ops);
         r->ops.clear();
@@ -1287,25 +1289,38 @@ static void sync_point(hipStream_t s, const char* what) {
 
 static bool capture_ops(DeviceDB::SearchGraph& G, const std::vector<StreamOp>& ops, hipStream_t st) {
     G.reset();
-    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+    auto fail = [&](const char* what, size_t i, hipError_t e) {
+        if (trace_on())
+            fprintf(stderr, "trace: search graph: %s failed at op %zu of %zu (kind %d): %s\n", what, i, ops.size(),
+                    i < ops.size() ? (int)ops[i].kind : -1, hipGetErrorString(e));
+        return false;
+    };
+    hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return fail("begin capture", 0, e);
     std::vector<hipGraphNode_t> nodes(ops.size(), nullptr);
     bool ok = true;
     for (size_t i = 0; i < ops.size() && ok; i++) {
         const StreamOp& op = ops[i];
-        ok = issue_op(op, true) == hipSuccess;
+        e = issue_op(op, true);
+        ok = e == hipSuccess || fail("capture", i, e);
         if (ok && (op.kind == StreamOp::kKernel || op.kind == StreamOp::kCopy || op.kind == StreamOp::kSet)) {
-            hipStreamCaptureStatus cs;
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
             const hipGraphNode_t* deps = nullptr;
             size_t nd = 0;
-            ok = hipStreamGetCaptureInfo_v2(op.stream, &cs, nullptr, nullptr, &deps, &nd) == hipSuccess &&
-                 cs == hipStreamCaptureStatusActive && nd == 1;
+            e = hipStreamGetCaptureInfo_v2(op.stream, &cs, nullptr, nullptr, &deps, &nd);
+            ok = (e == hipSuccess && cs == hipStreamCaptureStatusActive && nd == 1 && deps) ||
+                 fail(e != hipSuccess ? "capture info" : cs != hipStreamCaptureStatusActive ? "capture status"
+                                                                                             : "node count", i, e);
             if (ok) nodes[i] = deps[0];
         }
     }
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(st, &g);
-    ok = ok && e == hipSuccess && g;
-    if (ok) ok = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0) == hipSuccess;
+    e = hipStreamEndCapture(st, &g);
+    if (ok && (e != hipSuccess || !g)) ok = fail("end capture", ops.size(), e);
+    if (ok) {
+        e = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
+        if (e != hipSuccess) ok = fail("instantiate", ops.size(), e);
+    }
     if (!ok) {
         if (g) (void)hipGraphDestroy(g);
         G.exec = nullptr;
@@ -1315,17 +1330,37 @@ static bool capture_ops(DeviceDB::SearchGraph& G, const std::vector<StreamOp>& o
     G.g = g;
     G.ops = ops;
     G.nodes = std::move(nodes);
-    G.captures++;
     return true;
 }
 
-// returns 0: issued call by call, 1: captured, 2: replayed
-static uint32_t run_ops(DeviceDB& D, OpRecorder& rec, hipStream_t st) {
-    DeviceDB::SearchGraph& G = D.graph;
-    const std::vector<StreamOp>& ops = rec.ops;
-    if (ops.empty()) return 0;
-    bool same = G.exec && G.ops.size() == ops.size();
-    for (size_t i = 0; same && i < ops.size(); i++) same = same_shape(G.ops[i], ops[i]);
+// One segment of a search's operations (no timing record inside) as a
+// cached graph.  Returns 0: issued call by call, 1: captured, 2: replayed.
+static uint32_t run_segment(DeviceDB& D, const std::vector<StreamOp>& ops, hipStream_t st) {
+    auto shape_of = [&](const DeviceDB::SearchGraph& x) {
+        bool same = x.exec && x.ops.size() == ops.size();
+        for (size_t i = 0; same && i < ops.size(); i++) same = same_shape(x.ops[i], ops[i]);
+        return same;
+    };
+    DeviceDB::SearchGraph* pg = nullptr;
+    for (auto& x : D.graph.slot)
+        if (shape_of(x)) pg = &x;
+    bool same = pg != nullptr;
+    if (!pg) {
+        // a free slot, else the least recently used
+        for (auto& x : D.graph.slot)
+            if (!x.exec) {
+                pg = &x;
+                break;
+            }
+        if (!pg) {
+            pg = &D.graph.slot[0];
+            for (auto& x : D.graph.slot)
+                if (x.used < pg->used) pg = &x;
+        }
+    }
+    DeviceDB::SearchGraph& G = *pg;
+    const double t0 = now_ms();
+    uint32_t nset = 0;
     if (same) {
         for (size_t i = 0; same && i < ops.size(); i++) {
             const StreamOp &a = ops[i], &b = G.ops[i];
@@ -1339,27 +1374,60 @@ static uint32_t run_ops(DeviceDB& D, OpRecorder& rec, hipStream_t st) {
                 kp.kernelParams = p;
                 kp.sharedMemBytes = a.lds;
                 same = hipGraphExecKernelNodeSetParams(G.exec, G.nodes[i], &kp) == hipSuccess;
+                nset++;
             } else if (a.kind == StreamOp::kCopy && (a.dst != b.dst || a.src != b.src || a.bytes != b.bytes)) {
                 same = hipGraphExecMemcpyNodeSetParams1D(G.exec, G.nodes[i], a.dst, a.src, a.bytes, a.ck) == hipSuccess;
             }
         }
-        if (same) {
-            G.ops = ops;
-            G.replays++;
-        } else {
-            (void)hipGetLastError();
-        }
+        if (same) G.ops = ops;
+        else (void)hipGetLastError();
     }
     if (!same && !capture_ops(G, ops, st)) {
         // (this device searches call by call from now on)
-        G.reset();
-        G.broken = true;
+        D.graph.reset();
+        D.graph.broken = true;
         if (trace_on()) fprintf(stderr, "trace: search graph capture failed; direct launches\n");
         issue_all(ops);
         return 0;
     }
+    G.used = ++D.graph.clock;
+    const double t1 = now_ms();
     check(hipGraphLaunch(G.exec, st), "graph launch");
+    if (trace_on())
+        fprintf(stderr, "trace: search graph: segment of %zu ops, %s, %u kernel arguments set, %.1f us, launch %.1f us\n",
+                ops.size(), same ? "replayed" : "captured", nset, (t1 - t0) * 1e3, (now_ms() - t1) * 1e3);
     return same ? 2u : 1u;
+}
+
+// A recorded search: its timing records (kernel_ms: after the upload, after
+// the DP kernels' join) are issued on the stream as they are -- their
+// timestamps then mark exactly what they mark in a direct search -- and the
+// operations between them run as cached graphs (a lone operation directly).
+// Returns 0: issued call by call, 1: some segment captured, 2: all replayed.
+static uint32_t run_ops(DeviceDB& D, OpRecorder& rec, hipStream_t st) {
+    const std::vector<StreamOp>& ops = rec.ops;
+    if (ops.empty()) return 0;
+    uint32_t mode = 2;
+    bool any = false;
+    size_t i = 0;
+    while (i < ops.size()) {
+        if (ops[i].kind == StreamOp::kRecord && ops[i].timing) {
+            check(issue_op(ops[i], false), "event");
+            i++;
+            continue;
+        }
+        size_t j = i;
+        while (j < ops.size() && !(ops[j].kind == StreamOp::kRecord && ops[j].timing)) j++;
+        if (j - i == 1 || D.graph.broken) {
+            for (size_t x = i; x < j; x++) check(issue_op(ops[x], false), "stream operation");
+        } else {
+            const std::vector<StreamOp> seg(ops.begin() + i, ops.begin() + j);
+            mode = std::min(mode, run_segment(D, seg, st));
+            any = true;
+        }
+        i = j;
+    }
+    return any ? mode : 0u;
 }
 
 bool batch_pipelinable(size_t nqueries, size_t k) {
@@ -1978,9 +2046,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             tl = D.d_timeline;
         }
         check(op_record(ev_k0, st, true), "event");
-        // the long-entry streams fork from here: in a recorded search through
-        // an event of its own (ev_k0 becomes a timing node of the graph,
-        // which carries no dependency), otherwise through ev_k0 itself
+        // the long-entry streams fork here: in a recorded search through an
+        // event of its own, recorded inside the graph segment that follows
+        // (ev_k0 is issued on the stream between two graphs, run_ops)
         hipEvent_t fork_ev = ev_k0;
         if (op_recorder()) {
             fork_ev = D.ev_fork;
@@ -2608,6 +2676,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             op_recorder() = nullptr;
             out.graph = run_ops(D, rec, st);
         }
+        if (trace_on()) fprintf(stderr, "trace: search graph: eligible %d, ops %zu, mode %u\n", (int)use_graph, rec.ops.size(), out.graph);
         const double t_sync0 = now_ms();
         // filter_host 3: the filter's own stores, made visible by the end of
         // its dispatch -- an ordinary synchronisation, no copy, no spin

@@ -30,17 +30,26 @@ struct DeviceDB {
     hipStream_t stream = nullptr;
     hipEvent_t ev[9] = {};                // [8]: the int32 tier's end when it runs beside the filter
     hipEvent_t ev_fork = nullptr;         // a recorded search's fork to the long-entry streams
-    // the last graph-eligible search's stream operations as an instantiated
-    // HIP graph (engine.cpp run_ops): replayed while the next search issues
-    // the same operations, its changed arguments set on their nodes
+    // graph-eligible searches' stream operations as instantiated HIP graphs
+    // (engine.cpp run_ops), a few launch plans at once (least recently used
+    // replaced): a search whose operations have the shape of a cached graph's
+    // replays it with its changed arguments set on the nodes
     struct SearchGraph {
         hipGraph_t g = nullptr;
         hipGraphExec_t exec = nullptr;
         std::vector<StreamOp> ops;
         std::vector<hipGraphNode_t> nodes;   // per op: its node (kernels, copies, sets)
-        bool broken = false;                 // capture or instantiation failed once: direct from then on
-        uint64_t captures = 0, replays = 0;
+        uint64_t used = 0;
         void reset();
+    };
+    static constexpr size_t kGraphs = 8;
+    struct SearchGraphs {
+        SearchGraph slot[kGraphs];
+        bool broken = false;                 // a capture or instantiation failed: call by call from then on
+        uint64_t clock = 0;
+        void reset() {
+            for (auto& x : slot) x.reset();
+        }
     } graph;
     EntryMeta meta;
     uint32_t ngroups = 0;

@@ -8,10 +8,11 @@ OpRecorder*& op_recorder() {
     return r;
 }
 
-// capturing: inside a stream capture, a timing record becomes an event
-// record node (its timestamp is taken when the graph runs); the other
-// records and waits only carry the dependencies between the streams
+// (inside a stream capture HIP turns an event record into an event record
+// node -- its timestamp is taken when the graph runs, tools/graph_probe.hip --
+// and a wait on it into the dependency between the streams)
 hipError_t issue_op(const StreamOp& op, bool capturing) {
+    (void)capturing;
     switch (op.kind) {
     case StreamOp::kKernel: {
         void* p[32];
@@ -25,8 +26,7 @@ hipError_t issue_op(const StreamOp& op, bool capturing) {
     case StreamOp::kSet:
         return hipMemsetAsync(op.dst, op.value, op.bytes, op.stream);
     case StreamOp::kRecord:
-        return capturing && op.timing ? hipEventRecordWithFlags(op.event, op.stream, hipEventRecordExternal)
-                                      : hipEventRecord(op.event, op.stream);
+        return hipEventRecord(op.event, op.stream);
     case StreamOp::kWait:
         return hipStreamWaitEvent(op.stream, op.event, 0);
     }

@@ -399,12 +399,13 @@ def _split_worker(rank, world, port, outdir):
 
 
 class _FakeLib:
-    """The library calls bench.drop_in makes, recorded (no GPU): each search
-    'runs' on every selected slot; slot s takes (1 + s) ms of kernel."""
+    """The library calls bench.drop_in / drop_in_measure make, recorded (no
+    GPU): init_db reads SSA_AMD_DEVICES as the library does; each search
+    'runs' on every slot; slot s takes (1 + s) ms of kernel."""
     AMINOACID, NUCLEOTIDE, FORWARD_STRAND, MATRIX_BUILDIN, READ_FROM_STRING, SW = 0, 1, 1, 2, 1, 0
 
-    def __init__(self):
-        self.calls, self.devices, self.searches, self.records = [], [], 0, None
+    def __init__(self, env=None):
+        self.calls, self.devices, self.searches, self.records, self.env = [], [], 0, None, env or {}
 
     def __getattr__(self, name):        # configuration calls: recorded only
         return lambda *a: self.calls.append((name,) + a)
@@ -412,14 +413,13 @@ class _FakeLib:
     def ssa_exit(self):
         self.calls.append(("ssa_exit",))
 
-    def set_devices(self, devs):
-        self.calls.append(("set_devices", list(devs)))
-        self.devices = list(devs)
-        return 0
-
     def init_db(self, path):
         self.records = open(path).read().count(">")
+        self.devices = [int(x) for x in self.env.get("SSA_AMD_DEVICES", "0").split(",")]
         self.calls.append(("init_db",))
+
+    def get_devices(self):
+        return list(self.devices)
 
     def align_free(self, q, k, width, algo):
         self.searches += 1
@@ -437,7 +437,9 @@ class _FakeLib:
 
 
 def _dropin_worker(rank, world, port, outdir):
-    """One rank of bench.drop_in over gloo with the fake library."""
+    """One rank of bench.drop_in over gloo with the fake library; rank 0's
+    child process is stood in for by drop_in_measure on a fake library that
+    sees the child's environment."""
     import argparse
     import json
     import sys
@@ -449,30 +451,43 @@ def _dropin_worker(rank, world, port, outdir):
     import bench
     job = bench.Job(rank, world, dist, "cpu", "gloo")
     job.dev_index = 0
-    args = argparse.Namespace(n_gpus=1, steps=4, north_star_steps=None, k=10, drop_in_seqs=3000, cpu_seconds=1.0)
+    args = argparse.Namespace(n_gpus=1, steps=4, north_star_steps=None, k=10, drop_in_seqs=3000, cpu_seconds=1.0,
+                              option=["graph=1"])
     lib = _FakeLib()
-    rec = bench.drop_in(lib, args, job)
+    child = {}
+
+    def runner(cmd, env):
+        child.update(cmd=cmd, env={k: env[k] for k in ("SSA_AMD_DEVICES",) if k in env},
+                     ranked=[k for k in ("RANK", "WORLD_SIZE", "MASTER_PORT") if k in env])
+        clib = _FakeLib(env)
+        rec = bench.drop_in_measure(clib, args)
+        child.update(calls=[c[0] for c in clib.calls], records=clib.records, searches=clib.searches)
+        return rec
+    rec = bench.drop_in(lib, args, job, runner=runner)
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
-        json.dump({"rec": rec, "calls": [list(c[:1]) + [x for x in c[1:] if isinstance(x, (int, list))]
-                                         for c in lib.calls], "records": lib.records,
-                   "searches": lib.searches}, f)
+        json.dump({"rec": rec, "calls": [c[0] for c in lib.calls], "searches": lib.searches, "child": child}, f)
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_drop_in_record_on_gloo_rehearsal(tmp_path, world):
     """The N > 1 line's drop_in record (bench.drop_in): ranks != 0 release
-    their device DBs and wait; rank 0 opens the north-star DB (its first
-    3000 IDs here), selects one device slot per rank -- a rehearsal on one
-    GPU puts them all on device 0 -- times free_alignment(sw_align(...)) and
-    reports the per-slot kernel / search split; then it returns to its own
-    device."""
+    their device DBs and wait; rank 0 releases its own and runs a child
+    process (bench.py --drop-in-child) with SSA_AMD_DEVICES naming one device
+    slot per rank -- a rehearsal on one GPU puts them all on device 0 -- and
+    no rank variables; the child, an unchanged caller (no device selection of
+    its own), opens the north-star DB (its first 3000 IDs here), times
+    free_alignment(sw_align(...)) and reports the per-slot kernel / search
+    split."""
     import json
     mp.spawn(_dropin_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     r0 = json.load(open(tmp_path / "rank0.json"))
-    d = r0["rec"]
-    assert d["devices"] == [0] * world and d["slots"] == world
-    assert d["db_seqs"] == 3000 and r0["records"] == 3000 and d["steps"] == 4
+    d, ch = r0["rec"], r0["child"]
+    assert "--drop-in-child" in ch["cmd"] and ["--option", "graph=1"] == ch["cmd"][-2:]
+    assert ch["env"]["SSA_AMD_DEVICES"] == ",".join(["0"] * world) and ch["ranked"] == []
+    assert "set_device" not in ch["calls"] and "set_devices" not in ch["calls"]
+    assert d["devices"] == [0] * world and d["slots"] == world and d["devices_requested"] == [0] * world
+    assert d["db_seqs"] == 3000 and ch["records"] == 3000 and d["steps"] == 4
     assert d["cells_per_step"] == d["db_residues"] * 400
     assert d["slot_kernel_ms"] == [1.0 + s for s in range(world)]
     assert d["slot_search_ms"] == [1.25 + s for s in range(world)]
@@ -481,13 +496,22 @@ def test_bench_drop_in_record_on_gloo_rehearsal(tmp_path, world):
     assert sp["search"] == 0.5 + world and sp["merge_and_rest"] == 0.25
     assert abs(sp["step"] - d["ms_per_step"]) < 1e-3 and d["value"] > 0
     assert d["top_hit"] == [100, 0] and "topk_vs_reference" not in d      # (a 3000-ID slice: no fixture)
-    assert r0["searches"] == 4 + 2                                            # warm-up, 4 timed, the result
-    names = [c[0] for c in r0["calls"]]
-    assert names[0] == "ssa_exit" and ["set_devices", [0] * world] in r0["calls"]
-    assert r0["calls"][-2:] == [["set_devices", []], ["set_device", 0]]
+    assert ch["searches"] == 4 + 2                                            # warm-up, 4 timed, the result
+    assert r0["calls"] == ["ssa_exit"] and r0["searches"] == 0
     for r in range(1, world):
         rr = json.load(open(tmp_path / f"rank{r}.json"))
-        assert rr["rec"] is None and rr["calls"] == [["ssa_exit"]] and rr["searches"] == 0
+        assert rr["rec"] is None and rr["calls"] == ["ssa_exit"] and rr["searches"] == 0 and rr["child"] == {}
+
+
+def test_bench_drop_in_child_failure_is_reported():
+    """A failing child becomes the record's error, never the line's end."""
+    import sys
+    sys.path.insert(0, os.path.dirname(BENCH))
+    import bench
+    rec = bench._run_child([sys.executable, "-c", "import sys; sys.stderr.write('boom'); sys.exit(3)"], dict(os.environ))
+    assert rec["error"].endswith("status 3") and rec["stderr_tail"] == "boom"
+    rec = bench._run_child([sys.executable, "-c", "print('{\"value\": 5}')"], dict(os.environ))
+    assert rec == {"value": 5}
 
 
 @pytest.mark.parametrize("world", [2, 4])

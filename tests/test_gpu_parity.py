@@ -877,13 +877,18 @@ def test_search_graph_replays_exactly():
     M = TABLES["matrices"][NAMES.index("blosum62")].copy()
     ids = np.arange(len(seqs), dtype=np.uint64)
     configure(False, ("builtin", "blosum62"), -11, -1)
+    S.set_option("counters", 0)          # (counted searches run call by call)
     with tempfile.TemporaryDirectory() as tmp:
         S.init_db(_write_db(tmp, db, doff))
         qs = {n: syn.protein_query(n, 900 + n) for n in (60, 250, 400)}
         qq = {n: S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q)) for n, q in qs.items()}
         exp = {(n, a): po.scores(a, q, db, doff, M, -11, -1) for n, q in qs.items() for a in (S.SW, S.NW)}
-        order = [(400, S.SW, 10)] * 3 + [(60, S.SW, 10), (400, S.SW, 10), (250, S.NW, 64), (250, S.NW, 64),
-                                         (400, S.SW, 1), (400, S.SW, 64), (60, S.NW, 10), (60, S.NW, 10)]
+        # each plan three times (a plan's first search may also build its
+        # pair-row stream, a one-time operation: its shape is the plan's from
+        # the second search on), then each again after the others (four plans
+        # cached), then k = 1 (the same kernels as k = 10, other arguments)
+        order = ([(400, S.SW, 10)] * 3 + [(60, S.SW, 10)] * 3 + [(250, S.NW, 64)] * 3
+                 + [(400, S.SW, 10), (60, S.SW, 10), (250, S.NW, 64), (400, S.SW, 1), (60, S.NW, 10)])
         try:
             S.set_option("long_groups", 2)
             got = {}
@@ -899,10 +904,14 @@ def test_search_graph_replays_exactly():
             assert [x[0] for x in got[1]] == [x[0] for x in got[0]]
             modes = [x[1] for x in got[1]]
             assert all(m == 0 for _, m, _ in got[0]), [x[1] for x in got[0]]
-            assert modes[0] in (1, 2) and modes[1] == 2 and modes[2] == 2, modes
-            assert modes[4] in (1, 2) and modes[6] == 2 and modes[10] == 2, modes
+            print("graph modes", modes, "kernel ms", [round(x[2], 3) for x in got[1]], [round(x[2], 3) for x in got[0]])
+            assert modes[0] == 1 and min(modes) >= 1, str(modes)
+            assert [modes[i] for i in (2, 5, 8, 10, 11, 12)] == [2] * 6, str(modes)
+            # (a capturing search's kernel_ms also holds the capture, which
+            # runs between its two timing records)
             for (h1, m1, k1), (h0, m0, k0) in zip(got[1], got[0]):
-                assert 0 < k1 and 0.5 * k0 < k1 < 2.0 * k0 + 0.05, (k1, k0)
+                if m1 == 2:
+                    assert 0 < k1 and 0.75 * k0 < k1 < 1.33 * k0 + 0.05, (k1, k0)
         finally:
             S.set_option("graph", 1)
             S.set_option("long_groups", -1)
