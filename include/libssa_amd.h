@@ -140,10 +140,11 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "filter_prefix_regs" 1|0  the top-k filter's block scan with its states in registers and
  *                        merges at the list width k needs, for DBs of <= 256 filter blocks
  *                        (default), or always the general scan
- *   "graph" 1|0          1 (default): a single-view search with the device filter and no overflow
- *                        counters runs as a cached HIP graph -- captured once per launch plan, replayed
- *                        with the changed kernel arguments set on their nodes (stats graph); 0: every
- *                        stream operation issued on its own
+ *   "graph" 0|1          1: a single-view search with the device filter and no overflow counters runs
+ *                        as cached HIP graphs -- the operations between its two timing records captured
+ *                        once per launch plan, replayed with the changed kernel arguments set on their
+ *                        nodes (stats graph); 0 (default: the graphs measured slower than the direct
+ *                        calls): every stream operation issued on its own
  *   "upload_kernel" 1|0  1 (default): the per-search upload block (matrix, boundary, query) is read
  *                        from pinned host memory by a kernel on the search's stream; 0: a
  *                        copy-engine transfer (hipMemcpyAsync)

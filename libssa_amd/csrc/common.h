@@ -44,8 +44,9 @@ struct Config {
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
     int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
     int long16 = 1;                       // SW long entries on packed 16-bit patterns (long16_kernel) when exact
-    int graph = 1;                        // 1: the usual single-view search runs as a cached HIP graph (engine.cpp
-                                          // run_ops); 0: every operation issued on its own
+    int graph = 0;                        // 1: the usual single-view search runs as cached HIP graphs (engine.cpp
+                                          // run_ops; measured slower than the direct calls on ROCm 7.2,
+                                          // profiles/r06/graph); 0 (default): every operation issued on its own
     int upload_kernel = 1;                // 1: the per-search upload block is read from pinned memory by a kernel
                                           // on the search's stream instead of a copy-engine transfer (-14 us
                                           // between searches, profiles/r05/host_gap/kgap_upk*.txt)

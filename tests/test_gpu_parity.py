@@ -857,7 +857,7 @@ def test_filter_host_with_side_tier_overflow():
 
 
 def test_search_graph_replays_exactly():
-    """Option graph (default 1): the usual search's stream operations --
+    """Option graph 1 (default 0): the usual search's stream operations --
     upload, tables, long-entry kernels on their own streams, the pair kernel
     with strip parts, the filter, the result's copy -- are captured once per
     launch plan into a HIP graph and replayed with the changed arguments (gate
@@ -913,7 +913,7 @@ def test_search_graph_replays_exactly():
                 if m1 == 2:
                     assert 0 < k1 and 0.75 * k0 < k1 < 1.33 * k0 + 0.05, (k1, k0)
         finally:
-            S.set_option("graph", 1)
+            S.set_option("graph", 0)
             S.set_option("long_groups", -1)
         for q in qq.values():
             S.free_sequence(q)

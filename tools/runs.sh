@@ -150,6 +150,27 @@ run_kgap() (
     python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -2 "$OUT/gap.txt"
 )
 
+run_nsslice() (
+    # the north-star N = 8 rank-0 slice on one GPU (the first 1.25 M IDs of
+    # the 10 M DB): end to end vs kernel (5 x 20 steps) and the kernel trace's
+    # per-search gap
+    mkdir -p gpurun_out/$R/nsslice
+    for i in 1 2 3 4 5; do
+        timeout -k 10 300 python bench.py --config north_star --seqs 1250000 --steps 20 --warmup 3 --no-north-star \
+            --no-cpu-baseline "$@" > gpurun_out/$R/nsslice/run_$i.json 2> gpurun_out/$R/nsslice/run_$i.err \
+            || { tail -20 gpurun_out/$R/nsslice/run_$i.err; exit 1; }
+    done
+    python - <<'PYEOF'
+import json, glob, statistics as st, os
+R = os.environ.get("RUN", "r6")
+v, k = [], []
+for f in sorted(glob.glob(f"gpurun_out/{R}/nsslice/run_*.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    v.append(d["value"]); k.append(d["kernel"]["kernel_gcups"])
+print("nsslice median end-to-end", st.median(v), "kernel", st.median(k), "gap %", round(100 * (1 - st.median(v) / st.median(k)), 3), v)
+PYEOF
+)
+
 run_final() (
     # the default bench line (python bench.py: C2 headline, north_star,
     # cpu_baseline) under rocprofv3 --kernel-trace --stats: the summary whose
