@@ -810,16 +810,17 @@ def _run_child(cmd, env, timeout=900):
 
 def drop_in(S, args, job, runner=None):
     """N > 1, after the multi-process records: the drop-in path, measured.
-    Ranks != 0 release their device DBs (ssa_exit) and wait at a barrier;
-    rank 0 releases its own and starts `bench.py --drop-in-child` with
+    Ranks != 0 release their device DBs (ssa_exit) and end (no collective
+    follows); rank 0 releases its own and starts `bench.py --drop-in-child` with
     SSA_AMD_DEVICES listing one device slot per rank (a rehearsal's ranks
     share GPUs, so do its slots) -- a process of its own, so that whatever the
     single-process multi-GPU path does cannot take the multi-process line
     down with it (its failure becomes the record's "error").  Returns rank
     0's record (None elsewhere)."""
     if job.rank != 0:
+        # (no barrier: a rank waiting in an RCCL barrier keeps a spinning
+        # collective kernel on its GPU, which the child then shares)
         S.ssa_exit()
-        job.dist.barrier()
         return None
     S.ssa_exit()
     n_gpus = max(1, args.n_gpus)
@@ -839,7 +840,6 @@ def drop_in(S, args, job, runner=None):
     rec = (runner or _run_child)(cmd, env)
     rec["child_wall_s"] = round(time.time() - t0, 1)
     rec["devices_requested"] = devices
-    job.dist.barrier()
     return rec
 
 

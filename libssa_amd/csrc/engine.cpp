@@ -1410,8 +1410,6 @@ static uint32_t run_ops(DeviceDB& D, OpRecorder& rec, hipStream_t st) {
     uint32_t mode = 2;
     bool any = false;
     size_t i = 0;
-    // (option graph 2: the whole sequence one graph, timing records inside)
-    if (cfg().graph == 2 && !D.graph.broken) return run_segment(D, ops, st);
     while (i < ops.size()) {
         if (ops[i].kind == StreamOp::kRecord && ops[i].timing) {
             check(issue_op(ops[i], false), "event");
@@ -2674,7 +2672,6 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         if (parts_used && !perr_in_header)
             check(op_copy(h_perr, gate + 2, 4, hipMemcpyDeviceToHost, st), "D2H part status");
         out.graph = 0;
-        const double t_launch = now_ms();
         if (op_recorder()) {
             op_recorder() = nullptr;
             out.graph = run_ops(D, rec, st);
@@ -2866,17 +2863,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 if (ind) (*indep)[vv].kernel_ms = t;
             }
         } else {
-            // (option graph 2, an experiment: the timing records are captured
-            // inside the one graph, whose events do not time; then the host's
-            // time from the launch to the end of the synchronisation)
-            if (out.graph && C.graph == 2) {
-                if (hipEventElapsedTime(&t, D.ev[0], D.ev[1]) != hipSuccess) {
-                    (void)hipGetLastError();
-                    t = (float)(t_post0 - t_launch);
-                }
-            } else {
-                check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
-            }
+            check(hipEventElapsedTime(&t, D.ev[0], D.ev[1]), "elapsed");
             kms += t;
         }
         if (!lean || side_tier) {

@@ -472,7 +472,7 @@ def _dropin_worker(rank, world, port, outdir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_drop_in_record_on_gloo_rehearsal(tmp_path, world):
     """The N > 1 line's drop_in record (bench.drop_in): ranks != 0 release
-    their device DBs and wait; rank 0 releases its own and runs a child
+    their device DBs and end; rank 0 releases its own and runs a child
     process (bench.py --drop-in-child) with SSA_AMD_DEVICES naming one device
     slot per rank -- a rehearsal on one GPU puts them all on device 0 -- and
     no rank variables; the child, an unchanged caller (no device selection of
