@@ -59,15 +59,16 @@ from libssa_amd import workloads as W  # noqa: E402
 
 CONFIGS = W.CONFIGS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PEAK_CLOCK_GHZ = 2.4           # MI355X_MICROARCH.md: the engine's peak clock (the VALU issue ceiling)
 
 
-# The VALU issue roofline's inputs -- VALU lane-instructions per cell over a
-# search's DP kernels and the effective clock -- are PMC measurements of the
-# exact build and workload (tools/profile_pmc.sh -> tools/traffic_from_pmc.py
+# The VALU issue roofline's measured input -- VALU lane-instructions per cell
+# over a search's DP kernels (with the pass's own clock, reported beside) -- is
+# a PMC measurement of the exact build and workload (tools/profile_pmc.sh -> tools/traffic_from_pmc.py
 # -> profiles/traffic.json, filed under the workload key and the kernel-source
 # hash, libssa_amd/workloads.py kernel_src_hash); a line whose build hashes
-# differently reports them null with roofline.traffic_stale (rounds 1-5 kept
-# them in constant tables here: profiles/r0*/pmc_*).
+# differently reports it null with roofline.traffic_stale (rounds 1-5 kept it
+# in a constant table here: profiles/r0*/pmc_*).
 # share of those that are full-rate v_add_u32 (2.5 cycles per wave64
 # instruction per SIMD in isolation; the packed/VOP3 rest 4.17,
 # profiles/r01/ubench_valu_rates4.txt); from the DP loop's ISA census
@@ -949,14 +950,16 @@ def main():
     # VALU issue roofline: VOP3/VOP3P instructions issue at
     # 4.17 cycles per wave64 instruction per SIMD, v_add_u32 at 2.5 (measured
     # in isolation: profiles/r01/ubench_valu_rates4.txt); instructions per
-    # cell and the clock from this build's PMC pass of this workload
+    # cell from this build's PMC pass of this workload; the clock is the
+    # engine's peak (a profiled pass runs slower, MI355X_MICROARCH.md: its
+    # clock is reported beside, not used)
     kkey = (st["kernel"], st["strip_rows"])
-    instr_per_cell, clock = pf["valu_instr_per_cell"], pf["clock_ghz"]
+    instr_per_cell = pf["valu_instr_per_cell"]
     if args.strip_np != 16:
         instr_per_cell = None
     fast = VALU_FAST_SHARE.get(kkey, 0.0)
     issue_cycles = (1.0 - fast) * 4.17 + fast * 2.5
-    valu_bound = (1024 * clock * 1e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell and clock else None
+    valu_bound = (1024 * PEAK_CLOCK_GHZ * 1e9 / issue_cycles * 64 / instr_per_cell) if instr_per_cell else None
     out = {
         "metric": "GCUPS (SW int16, 400aa query vs synthetic DB) at 1/2/4/8 MI355X; top-k score bit-exact",
         "value": round(gcups, 2),
@@ -985,7 +988,8 @@ def main():
                      "binding": {"bound": "valu_issue",
                                  "achieved": round(cells_local / (kavg * 1e-3) / 1e9, 2),
                                  "peak": round(valu_bound / 1e9, 1) if valu_bound else None, "unit": "GCUPS",
-                                 "clock_ghz": clock, "valu_instr_per_cell": instr_per_cell,
+                                 "clock_ghz": PEAK_CLOCK_GHZ, "pmc_pass_clock_ghz": pf["clock_ghz"],
+                                 "valu_instr_per_cell": instr_per_cell,
                                  "frac": (cells_local / (kavg * 1e-3)) / valu_bound if valu_bound else None}},
         "kernel": {"name": st["kernel"], "avg_ms": round(kavg, 4),
                    "kernel_gcups": round(cells_local / (kavg * 1e-3) / 1e9, 2),

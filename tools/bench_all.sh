@@ -17,6 +17,7 @@ run c5share1m --config c5 --seqs 1000000 --steps 3 --no-cpu-baseline --no-north-
 run c5share --config c5 --seqs 6250000 --steps 2 --warmup 1 --no-north-star &&
 run ref --config ref --steps 10 --no-cpu-baseline --no-north-star &&
 run sprot --config sprot --steps 10 --no-cpu-baseline --no-north-star &&
+run u28 --alphabet uniform28 --steps 10 --no-cpu-baseline --no-north-star &&
 run c4full --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-north-star &&
 run north_star --config north_star --steps 5 --warmup 1 --no-cpu-baseline --no-north-star &&
 run c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline --no-north-star
