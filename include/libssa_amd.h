@@ -100,8 +100,11 @@ typedef struct {
  *   SSA_AMD_DEVICES = all (also: unset or empty) | current | 0,2,...
  * -- every visible device, the current HIP device only, or this list
  * (repeats allowed: several slots on one device).  Several devices work as
- * ssa_amd_set_devices below.  An explicit ssa_amd_set_device(s) always wins
- * (one rank per GPU: ssa_amd_set_device(local_rank)). */
+ * ssa_amd_set_devices below.  set_thread_count(n) (libssa.h: the reference's
+ * number of search workers) caps that list at its first n devices (0: all),
+ * so the reference's thread sweeps become device sweeps.  An explicit
+ * ssa_amd_set_device(s) always wins (one rank per GPU:
+ * ssa_amd_set_device(local_rank)) and no thread count changes it. */
 int ssa_amd_device_count( void );
 void ssa_amd_set_device( int device );
 void ssa_amd_set_id_offset( size_t offset );

@@ -25,6 +25,23 @@ p_query query_from_file(const char* path);
 
 namespace {
 
+// The environment's device list as the search uses it: its first
+// set_thread_count() devices -- the reference's thread count is its number of
+// search workers (thread_pool.c:39-47), a device slot's analogue here; 0 (the
+// default) = all of them.  An explicit ssa_amd_set_device(s) is left alone.
+void refresh_env_devices() {
+    Config& C = cfg();
+    if (C.device_chosen || !C.device_env_read || C.env_devices.empty()) return;
+    std::vector<int> d = C.env_devices;
+    if (C.thread_count > 0 && d.size() > C.thread_count) d.resize(C.thread_count);
+    if (d.size() > 1) {
+        C.devices = d;
+    } else {
+        C.devices.clear();
+        C.device = d[0];
+    }
+}
+
 // SSA_AMD_DEVICES (include/libssa_amd.h), applied once -- at the first
 // init_db or device query -- unless the caller chose devices itself.  The
 // reference's default is every core (src/util/thread_pool.c:39-47); here it
@@ -42,7 +59,11 @@ void apply_device_env() {
     std::vector<int> devs;
     if (!e || !*e || !strcmp(e, "all")) {
         for (int i = 0; i < count && devs.size() < kMaxSlots; i++) devs.push_back(i);
-        if (devs.size() > 1) C.devices = devs;   // (one device: the current-device path, unchanged)
+        // (one device: the current-device path, unchanged)
+        if (devs.size() > 1) {
+            C.env_devices = devs;
+            refresh_env_devices();
+        }
         return;
     }
     if (!strcmp(e, "current")) return;
@@ -62,8 +83,8 @@ void apply_device_env() {
             return;
         }
     }
-    if (devs.size() == 1) C.device = devs[0];
-    else if (devs.size() > 1) C.devices = devs;
+    C.env_devices = devs;
+    refresh_env_devices();
 }
 
 // Persistent per-slot host threads for multi-device searches (SURVEY.md §8b
@@ -376,7 +397,12 @@ void set_chunk_size(size_t size) {
     }
     cfg().chunk_size = size;
 }
-void set_thread_count(size_t count) { cfg().thread_count = count; }
+// (libssa.c:58-60: the number of search workers; here it caps the device
+// slots an unchanged caller gets from SSA_AMD_DEVICES / all devices)
+void set_thread_count(size_t count) {
+    cfg().thread_count = count;
+    refresh_env_devices();
+}
 
 // ------------------------------------------------------------ initialisation
 void init_score_matrix(int mode, const char* m) {

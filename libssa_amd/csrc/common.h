@@ -30,6 +30,8 @@ struct Config {
     std::vector<int> devices;             // ssa_amd_set_devices: shard the DB over these
     bool device_chosen = false;           // the caller called ssa_amd_set_device(s): SSA_AMD_DEVICES is not read
     bool device_env_read = false;         // SSA_AMD_DEVICES was applied (at the first init_db)
+    std::vector<int> env_devices;         // the devices SSA_AMD_DEVICES (or its default, all) lists; the search
+                                          // uses the first set_thread_count() of them (api.cpp refresh_env_devices)
     size_t id_offset = 0;                 // global ID of local record 0
     uint64_t db_generation = 0;           // bumped by init_db
     // tuning knobs (ssa_amd_set_option)

@@ -1664,10 +1664,10 @@ def test_reference_cli_links_and_matches(algo, bits):
     assert got == [tuple(x) for x in case[algo.lower() + "_64"]]
 
 
-def _cli(db, query, algo, bits, k, devices):
+def _cli(db, query, algo, bits, k, devices, threads=4):
     import subprocess
     env = dict(os.environ, SSA_AMD_DEVICES=devices)
-    r = subprocess.run([CLI, "-N", "4", "-O", "-11", "-E", "-1", "-M", "BLOSUM62", "-i", query, "-d", db,
+    r = subprocess.run([CLI, "-N", str(threads), "-O", "-11", "-E", "-1", "-M", "BLOSUM62", "-i", query, "-d", db,
                         "-c", str(k), "-t", algo, "-b", str(bits), "-s", "AVX2"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, (devices, r.stderr[-2000:])
@@ -1704,13 +1704,20 @@ def test_reference_cli_on_several_devices_via_env(algo, tmp_path):
             assert len(book1) == 1 and len(book3) == 3, (book1, book3)
             seqs = [int(ln.rsplit(" ", 1)[1]) for ln in book3]
             assert sum(seqs) == int(book1[0].rsplit(" ", 1)[1]), (book1, book3)
+    # the CLI's -N (set_thread_count, the reference's number of search
+    # workers) caps the listed devices: -N 2 of 0,0,0 runs two slots
+    two = _cli(big, query, algo, 16, 500, "0,0,0", threads=2)
+    assert [ln for ln in two.splitlines() if "Processed chunks" not in ln] == \
+        [ln for ln in _cli(big, query, algo, 16, 500, "current").splitlines() if "Processed chunks" not in ln]
+    assert sum("Processed chunks" in ln for ln in two.splitlines()) == 2
 
 
 def test_device_env_selects_slots(tmp_path):
     """SSA_AMD_DEVICES, read at the first init_db unless the caller chose
     devices: all / unset / empty = every visible device, current = the
     current one, a list (repeats allowed), invalid lists fall back to the
-    current device with an error; an explicit ssa_amd_set_device wins."""
+    current device with an error; set_thread_count(n) caps the list at its
+    first n; an explicit ssa_amd_set_device(s) wins over both."""
     import subprocess
     import sys
     db = os.path.join(DATA, "test.fas")
@@ -1739,6 +1746,14 @@ def test_device_env_selects_slots(tmp_path):
         assert got == [0] and "SSA_AMD_DEVICES" in out, (bad, got, out)
     assert devs("0,0", pre="S.set_device(0); ")[0] == [0]
     assert devs("current", pre="S.set_devices([0, 0]); ")[0] == [0, 0]
+    # set_thread_count caps the listed devices, before or after init_db
+    assert devs("0,0,0", pre="S.set_thread_count(2); ")[0] == [0, 0]
+    assert devs("0,0,0", pre="S.set_thread_count(1); ")[0] == [0]
+    assert devs("0,0,0", pre="S.set_thread_count(7); ")[0] == [0, 0, 0]
+    got, _ = devs("0,0,0", pre="S.set_thread_count(2); S.init_db(%r); S.set_thread_count(0); " % db)
+    assert got == [0, 0, 0]
+    # ... but never an explicit choice
+    assert devs("0,0,0", pre="S.set_devices([0, 0, 0, 0]); S.set_thread_count(2); ")[0] == [0, 0, 0, 0]
 
 
 @pytest.mark.parametrize("gaps", [(0, 0), (-5, 0), (0, -1), (-1, -3), (-20, -7)])
