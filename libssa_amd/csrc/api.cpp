@@ -482,7 +482,14 @@ void ssa_exit(void) {
     cfg().db_generation++;
     for (size_t s = 0; s < kMaxSlots; s++) {
         DeviceDB& D = device_db(s);
-        if (D.device >= 0) D.release();
+        if (D.device < 0) continue;
+        // (a runtime already shut down -- ssa_exit from an atexit handler --
+        // leaves the memory to the process's end)
+        if (hipSetDevice(D.device) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        D.release();
     }
 }
 

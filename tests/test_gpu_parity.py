@@ -1712,6 +1712,33 @@ def test_reference_cli_on_several_devices_via_env(algo, tmp_path):
     assert sum("Processed chunks" in ln for ln in two.splitlines()) == 2
 
 
+def test_ssa_exit_releases_device_memory(tmp_path):
+    """ssa_exit (libssa.c:266-271 frees the reference's state and ends its
+    thread pool) also releases the device copies of the DB -- what bench.py's
+    drop_in record relies on before its child packs the north-star DB."""
+    import torch
+    codes, off = syn.protein_db(200_000, 77, lo=16, hi=2000)
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    free0 = torch.cuda.mem_get_info(0)[0]
+    S.prepare_db()
+    free1 = torch.cuda.mem_get_info(0)[0]
+    S.ssa_exit()
+    free2 = torch.cuda.mem_get_info(0)[0]
+    packed = free0 - free1
+    assert packed > int(off[-1]) * 4, (free0, free1)          # row buffer alone: 4 B per residue slot
+    assert free2 - free1 > 0.9 * packed, (free0, free1, free2)
+    # the library works again after it
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    S.init_db(_write_db(str(tmp_path), codes[:int(off[1000])], off[:1001]))
+    q = syn.protein_query(50, 3)
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    M = TABLES["matrices"][NAMES.index("blosum62")].copy()
+    exp = po.scores(S.SW, q, codes[:int(off[1000])], off[:1001], M, -11, -1)
+    assert [(h["score"], h["id"]) for h in S.sw_align(qq, 5, 16)] == po.topk(exp, np.arange(1000, dtype=np.uint64), 5)
+    S.free_sequence(qq)
+
+
 def test_device_env_selects_slots(tmp_path):
     """SSA_AMD_DEVICES, read at the first init_db unless the caller chose
     devices: all / unset / empty = every visible device, current = the

@@ -58,10 +58,11 @@ run_medians() (
         done
     done
     python - <<'EOF'
-import json, glob, statistics as st
+import json, glob, os, statistics as st
+R = os.environ.get("RUN", "r6")
 for cfg in ("c2", "ref", "sprot"):
     v, k = [], []
-    for f in sorted(glob.glob(f"gpurun_out/$R/medians/{cfg}_*.json")):
+    for f in sorted(glob.glob(f"gpurun_out/{R}/medians/{cfg}_*.json")):
         d = json.loads(open(f).read().strip().splitlines()[-1])
         v.append(d["value"]); k.append(d["kernel"]["kernel_gcups"])
     print(cfg, "median end-to-end", st.median(v), "kernel", st.median(k), v)
