@@ -1727,7 +1727,15 @@ def test_ssa_exit_releases_device_memory(tmp_path):
     free2 = torch.cuda.mem_get_info(0)[0]
     packed = free0 - free1
     assert packed > int(off[-1]) * 4, (free0, free1)          # row buffer alone: 4 B per residue slot
-    assert free2 - free1 > 0.9 * packed, (free0, free1, free2)
+    # (the runtime may keep part of what was freed for its own reuse)
+    assert free2 - free1 > 0.5 * packed, (free0, free1, free2)
+    # packing the same DB again takes no more than the first time: nothing leaked
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    S.prepare_db()
+    free3 = torch.cuda.mem_get_info(0)[0]
+    assert free3 > free1 - 0.05 * packed, (free0, free1, free2, free3)
+    S.ssa_exit()
     # the library works again after it
     configure(False, ("builtin", "blosum62"), -11, -1)
     S.init_db(_write_db(str(tmp_path), codes[:int(off[1000])], off[:1001]))
