@@ -157,6 +157,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "tail_rows4" 1|0     the pair kernel's last strip at 4-row granularity (default; SW 48-row and
  *                        NW 64/80-row strips, after a main strip), or 8-row (0)
  *   "long_prio" 1|0      long16 waves at raised issue priority over the pair waves (default 1)
+ *   "long_pad" 1|0       long-entry workgroups pad their LDS to the pair kernel's, so a finished one
+ *                        leaves a pair workgroup's hole (default 1; 0 measured -6 % on the Swiss-Prot form)
  *   "long_gate" 1|0|P    the pair kernel starts after the long-entry workgroups have (default 1;
  *                        0: no wait, the long-entry streams' priority alone orders them; 2..99:
  *                        after the first P % of them)

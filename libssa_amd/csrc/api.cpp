@@ -637,6 +637,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "lean_events")) cfg().lean_events = (int)value;
     else if (!strcmp(name, "long16_rows")) cfg().long16_rows = (int)value;
     else if (!strcmp(name, "long_gate")) cfg().long_gate = (int)value;
+    else if (!strcmp(name, "long_pad")) cfg().long_pad = (int)value;
     else if (!strcmp(name, "long_prio")) cfg().long_prio = (int)value;
     else if (!strcmp(name, "tail_rows4")) cfg().tail_rows4 = (int)value;
     else if (!strcmp(name, "tier_defer")) cfg().tier_defer = (int)value;

@@ -56,6 +56,8 @@ struct Config {
                                           // copy, only when the search has overflowed lanes
     int tail_rows4 = 1;                   // pair kernel tail strips at 4-row granularity (default heights)
     int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
+    int long_pad = 1;                     // 1: long-entry workgroups pad their LDS to the pair kernel's (a finished
+                                          // one leaves exactly a pair workgroup's hole); 0: their own LDS only
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry
                                           // workgroups have started (TableArgs::gate)
     int long16_rows = 1;                  // long16_kernel may leave up to 8 query rows to its row scan (LongArgs::extra16)

@@ -2138,7 +2138,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             }
             la.gate = gate;
             la.timeline = tl;
-            if (use_pair) la.lds_min = (uint32_t)pair_lds;
+            if (use_pair && C.long_pad) la.lds_min = (uint32_t)pair_lds;
             gate_base = gate_total;
             // (issued right after the tables kernel below: the host issues
             // the next GPU step first, and the tables kernel's gate holds the
@@ -2180,9 +2180,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 else if (long4 == long_groups) snprintf(lkname, sizeof lkname, "long32_w4_rl%d", rl4);
                 else snprintf(lkname, sizeof lkname, "long32_w4_rl%d+w1_rl%d", rl4, rl1);
             }
-            lds_long = std::max(pair_lds, rl16 > 0 ? long16_lds_bytes(la.alpha, rl16)
-                                                   : long4 > 0 ? long_lds_bytes(la.alpha, 4, rl4)
-                                                               : long_lds_bytes(la.alpha, 1, rl1));
+            lds_long = std::max(C.long_pad ? pair_lds : 0,
+                                rl16 > 0 ? long16_lds_bytes(la.alpha, rl16)
+                                         : long4 > 0 ? long_lds_bytes(la.alpha, 4, rl4) : long_lds_bytes(la.alpha, 1, rl1));
         }
         // the pair tables, then the long entries' launches: the tables kernel
         // runs while the host issues them, and its gate (block 0) holds the
