@@ -320,7 +320,8 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     S.counters = (bw == BIT_WIDTH_64 || counters_on(cfg())) ? 1 : 0;
     S.replay_ms = t2 - t1;
     S.search_ms = now_ms() - t0;
-    if (trace_on()) fprintf(stderr, "trace: run_search to device_search end %.3f, replay %.3f, total %.3f\n", t1 - t0, t2 - t1, S.search_ms);
+    if (trace_on()) fprintf(stderr, "trace: run_search on %zu device slots: to device_search end %.3f, replay %.3f, total %.3f\n",
+                            plan.size(), t1 - t0, t2 - t1, S.search_ms);
     S.total_searches++;
     S.total_kernel_ms += S.kernel_ms;
     S.total_search_ms += S.search_ms;

@@ -1712,6 +1712,51 @@ def test_reference_cli_on_several_devices_via_env(algo, tmp_path):
     assert sum("Processed chunks" in ln for ln in two.splitlines()) == 2
 
 
+BENCH_THREADS = os.path.join(os.path.dirname(po.__file__), "_ref", "benchmark_threads_amd")
+
+
+@pytest.mark.skipif(not os.path.exists(BENCH_THREADS), reason="reference benchmark not built (make -C oracle ref)")
+def test_reference_thread_sweep_becomes_device_slot_sweep(tmp_path):
+    """The reference's own thread-sweep benchmark (benchmark/src/
+    benchmark_threads.c + benchmark_util.c, compiled unchanged) on six listed
+    device slots: its set_thread_count(2, 3, 5, 6, 0, 0) sweep runs 2, 3, 5,
+    6, 6, 6 slots (0 = every listed device), each of its 360 searches (SW/NW x
+    8/16/64 bit x 10) completes, and it logs its 36 timing rows to
+    results/ as on the CPU.  Its DB and query paths are fixed
+    (data/uniprot_sprot.fasta, data/P18080): a 20000-entry synthetic protein
+    DB and the Q3ZAI3 query stand in (the reference's data/ files are not on
+    the GPU box)."""
+    import shutil
+    import subprocess
+    os.makedirs(tmp_path / "data")
+    os.makedirs(tmp_path / "results")
+    codes, off = syn.protein_db(20_000, 91, lo=8, hi=1200)
+    syn.write_fasta(str(tmp_path / "data" / "uniprot_sprot.fasta"), codes, off, False)
+    shutil.copy(os.path.join(DATA, "Q3ZAI3.fasta"), tmp_path / "data" / "P18080")
+    env = dict(os.environ, SSA_AMD_DEVICES="0,0,0,0,0,0", SSA_AMD_TRACE="1")
+    r = subprocess.run([BENCH_THREADS], cwd=str(tmp_path), capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [ln for ln in r.stdout.splitlines() if ln.startswith("P18080,")]
+    assert len(rows) == 36, r.stdout[-2000:]
+    expect = []
+    for t in (2, 3, 5, 6, 0, 0):
+        for algo in ("SW", "NW"):
+            for b in (8, 16, 64):
+                simd = "NO_SIMD" if b == 64 else "AVX2"
+                expect.append(f"P18080,{simd},{algo},{b}_bit,{t}_t")
+    assert [",".join(ln.split(",")[:5]) for ln in rows] == expect
+    for ln in rows:
+        times = [float(x) for x in ln.split(",")[5:]]
+        assert len(times) == 10 and all(0.0 < x < 30.0 for x in times), ln
+    slots = [int(ln.split(" on ")[1].split()[0]) for ln in r.stderr.splitlines()
+             if ln.startswith("trace: run_search on ")]
+    assert slots == [n for n in (2, 3, 5, 6, 6, 6) for _ in range(60)], slots[:80]
+    logs = os.listdir(tmp_path / "results")
+    assert len(logs) == 1 and logs[0].endswith("_threads")
+    with open(tmp_path / "results" / logs[0]) as f:
+        assert f.read().count("\n") == 36
+
+
 def test_ssa_exit_releases_device_memory(tmp_path):
     """ssa_exit (libssa.c:266-271 frees the reference's state and ends its
     thread pool) also releases the device copies of the DB -- what bench.py's
