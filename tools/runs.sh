@@ -48,6 +48,21 @@ run_pmc_shapes() (
     done
 )
 
+run_pmc_sprot() (
+    # the Swiss-Prot form's factors on one box: stats/valu/lds passes of the
+    # 20-letter ref shape, the 25-letter form without and with its length
+    # tail, each 25-letter case also with the rare-code merge (three pair
+    # workgroups per CU); summary by tools/pmc_shapes.py
+    for cfg in "ref:--config ref" "notail:--config sprot --long-tail 0" \
+               "notail_merge:--config sprot --long-tail 0 --option rare_merge=1" \
+               "sprot:--config sprot" "sprot_merge:--config sprot --option rare_merge=1"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        PASSES="stats valu lds" bash tools/profile_pmc.sh gpurun_out/$R/pmc_sprot/$name $args || exit 1
+        echo "$name done"
+    done
+    python3 tools/pmc_shapes.py gpurun_out/$R/pmc_sprot/* > gpurun_out/$R/pmc_sprot/summary.txt && cat gpurun_out/$R/pmc_sprot/summary.txt
+)
+
 run_medians() (
     # 5 x 20 steps of C2, ref, sprot (kernel and end-to-end TCUPS)
     mkdir -p gpurun_out/$R/medians
