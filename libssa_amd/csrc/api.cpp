@@ -277,6 +277,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
     ensure_device_db();
     const std::vector<SlotPlan> plan = device_plan();
     R.views = query_views(q);
+    host_mark("views");
     std::vector<SearchScores> sc(plan.size());
     std::vector<std::vector<Hit>> logs(plan.size());
     std::vector<double> slot_ms(plan.size(), 0.0);
@@ -296,6 +297,7 @@ void run_search(p_query q, int algo, size_t k, int bw, bool want_log, SearchResu
         });
     }
     const double t1 = now_ms();
+    host_mark("searched");
     TopK heap(k);
     if (plan.size() == 1) {
         replay(sc[0], device_db(0).meta, R.views, heap, want_log ? &R.hits : nullptr);
@@ -376,11 +378,27 @@ p_alignment_list build_list(const SearchResult& R) {
 }
 
 p_alignment_list align(p_query q, size_t k, int bw, int at, int algo) {
+    // (SSA_AMD_TRACE: the host's timeline of the call, from the previous
+    // call's return -- the caller's own time -- to this one's)
+    static double last_return = 0;
+    if (trace_on()) {
+        host_marks().clear();
+        host_mark("entry");
+    }
     test_configuration(q);
     SearchResult R;
     run_search(q, algo, k, bw, false, R);
     p_alignment_list L = build_list(R);
     if (at == COMPUTE_ALIGNMENT) compute_alignments(L, algo);   // align.cpp (aligner.c:163-181)
+    if (trace_on()) {
+        host_mark("return");
+        const auto& m = host_marks();
+        const double t0 = m.front().second;
+        fprintf(stderr, "trace: host us (entry at %.0f ns): caller %.1f", t0 * 1e6, last_return > 0 ? (t0 - last_return) * 1e3 : -1.0);
+        for (size_t i = 1; i < m.size(); i++) fprintf(stderr, ", %s %.1f", m[i].first, (m[i].second - t0) * 1e3);
+        fprintf(stderr, "\n");
+        last_return = now_ms();
+    }
     return L;
 }
 
@@ -407,6 +425,7 @@ void set_thread_count(size_t count) {
 
 // ------------------------------------------------------------ initialisation
 void init_score_matrix(int mode, const char* m) {
+    cfg().plan_gen++;
     if (mode == READ_FROM_FILE) matrix_from_file(m);
     else if (mode == READ_FROM_STRING) matrix_from_string(m);
     else if (mode == MATRIX_BUILDIN) matrix_builtin(m);
@@ -414,11 +433,15 @@ void init_score_matrix(int mode, const char* m) {
 }
 
 void init_gap_penalties(const int8_t gapO, const int8_t gapE) {
+    cfg().plan_gen++;
     cfg().gap_open = gapO;
     cfg().gap_extend = gapE;
 }
 
-void init_constant_scores(const int8_t p, const int8_t m) { matrix_constant(p, m); }
+void init_constant_scores(const int8_t p, const int8_t m) {
+    cfg().plan_gen++;
+    matrix_constant(p, m);
+}
 
 // MI355X: validates the NEW type and strands (the reference checks the old
 // global symtype twice, libssa.c:146-151, and so rejects any call made after
@@ -428,6 +451,7 @@ void init_symbol_translation(int type, int strands, int d_gencode, int q_gencode
     if (!gencode_valid(d_gencode)) fatal("Illegal database genetic code specified.");
     if (type < 0 || type > 4) fatal("Illegal symbol type specified.");
     if (strands < 1 || strands > 3) fatal("Illegal strands specified.");
+    cfg().plan_gen++;
     cfg().symtype = type;
     cfg().strands = strands;
     cfg().q_gencode = q_gencode;
@@ -612,6 +636,7 @@ size_t ssa_amd_translate(int db_side, const char* nt_codes, size_t len, int stra
 
 void ssa_amd_set_option(const char* name, long value) {
     if (!name) return;
+    cfg().plan_gen++;
     if (!strcmp(name, "strip_np")) cfg().strip_np = (int)value;
     else if (!strcmp(name, "force_wide")) cfg().force_wide = (int)value;
     else if (!strcmp(name, "sw_kernel")) cfg().sw_kernel = (int)value;
@@ -644,6 +669,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "tier_defer")) cfg().tier_defer = (int)value;
     else if (!strcmp(name, "upload_kernel")) cfg().upload_kernel = (int)value;
     else if (!strcmp(name, "graph")) cfg().graph = (int)value;
+    else if (!strcmp(name, "plan_cache")) cfg().plan_cache = (int)value;
     else if (!strcmp(name, "filter_prefix_regs")) set_filter_prefix_regs((int)value);
     else print_warning("unknown option %s", name);
 }

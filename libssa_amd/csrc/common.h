@@ -19,6 +19,9 @@ constexpr size_t kMaxSlots = 16;   // devices one process can search on
 
 // ------------------------------------------------------------------ config
 struct Config {
+    // bumped by every setter of the scoring or the options (api.cpp): the
+    // per-DB plan cache (engine.cpp cached_plan) keys on it
+    uint64_t plan_gen = 0;
     int output_mode = OUTPUT_WARNING;     // reference util.c:34
     size_t chunk_size = 1000;             // reference util.h:31 DEFAULT_CHUNK_SIZE
     size_t thread_count = 0;              // 0 = all host cores
@@ -56,7 +59,8 @@ struct Config {
                                           // copy, only when the search has overflowed lanes
     int tail_rows4 = 1;                   // pair kernel tail strips at 4-row granularity (default heights)
     int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
-    int long_pad = 1;                     // 1: long-entry workgroups pad their LDS to the pair kernel's (a finished
+    int long_pad = 1;
+    int plan_cache = 1;                   // engine.cpp cached_plan (0: plan every search)                     // 1: long-entry workgroups pad their LDS to the pair kernel's (a finished
                                           // one leaves exactly a pair workgroup's hole); 0: their own LDS only
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry
                                           // workgroups have started (TableArgs::gate)

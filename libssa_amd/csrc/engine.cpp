@@ -31,6 +31,16 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// SSA_AMD_TRACE: the host's timeline of one search (host_mark at the points
+// below, printed by api.cpp run_search relative to its entry)
+std::vector<std::pair<const char*, double>>& host_marks() {
+    thread_local std::vector<std::pair<const char*, double>> m;
+    return m;
+}
+void host_mark(const char* what) {
+    if (trace_on()) host_marks().emplace_back(what, now_ms());
+}
+
 void check(hipError_t e, const char* what) {
     if (e != hipSuccess) fatal("HIP error in %s: %s", what, hipGetErrorString(e));
 }
@@ -62,6 +72,7 @@ void DeviceDB::release() {
     // (the cached graph names the buffers freed below)
     graph.reset();
     graph.broken = false;
+    plans.reset();
     dfree(d_groups); dfree(d_res); dfree(d_rowbuf); dfree(d_lane_len); dfree(d_lane_out);
     dfree(d_scores); dfree(d_ovf); dfree(d_wide); dfree(d_qpt); dfree(d_upblk);
     dfree(d_work); dfree(d_order); dfree(d_lscratch); dfree(d_rscratch);
@@ -1220,6 +1231,55 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
     vp.qpt_words = qpt_words;
 }
 
+// plan_view's result for the last few (query, kind) pairs of a packed DB: a
+// search repeats its predecessor's plan when the query and every setting it
+// reads are unchanged (Config::plan_gen; the DB's own state is the
+// DeviceDB's, whose release() drops the cache) -- ~7 us of host time per
+// search on the path between two searches (profiles/r06/htrace)
+struct PlanCache {
+    struct Entry {
+        std::vector<uint8_t> seq;
+        uint64_t gen = 0, used = 0;
+        int np = 0;
+        bool nw = false, merge = false, batch = false;
+        ViewPlan vp;
+    };
+    std::vector<Entry> e;
+    uint64_t clock = 0;
+};
+
+static void cached_plan(DeviceDB& D, const QueryView& qv, bool nw, int np, ViewPlan& vp, bool allow_merge) {
+    if (!cfg().plan_cache) return plan_view(D, qv, nw, np, nullptr, vp, allow_merge);   // (option "plan_cache" 0)
+    if (!D.plans) D.plans = std::make_shared<PlanCache>();
+    PlanCache& P = *D.plans;
+    const uint64_t gen = cfg().plan_gen;
+    for (auto& x : P.e)
+        if (x.gen == gen && x.np == np && x.nw == nw && x.merge == allow_merge && !x.batch && x.seq.size() == qv.len &&
+            (qv.len == 0 || !memcmp(x.seq.data(), qv.seq, qv.len))) {
+            x.used = ++P.clock;
+            vp = x.vp;
+            return;
+        }
+    plan_view(D, qv, nw, np, nullptr, vp, allow_merge);
+    constexpr size_t kPlans = 4;
+    PlanCache::Entry* slot = nullptr;
+    if (P.e.size() < kPlans) {
+        slot = &P.e.emplace_back();
+    } else {
+        slot = &P.e[0];
+        for (auto& x : P.e)
+            if (x.used < slot->used) slot = &x;
+    }
+    slot->seq.assign(qv.seq, qv.seq + qv.len);
+    slot->gen = gen;
+    slot->np = np;
+    slot->nw = nw;
+    slot->merge = allow_merge;
+    slot->batch = false;
+    slot->used = ++P.clock;
+    slot->vp = vp;
+}
+
 // per entry the compact codes it holds and per code the entries holding it
 // (the rare-code merge's decision and flags), once per packed DB
 static void ensure_entry_masks(DeviceDB& D) {
@@ -1715,7 +1775,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // planned every query up front with shared bounds
         ViewPlan vpl;
         if (fused) vpl = fplans[v];
-        else plan_view(D, qv, nw, np, nullptr, vpl, allow_merge);
+        else cached_plan(D, qv, nw, np, vpl, allow_merge);
+        if (v == 0) host_mark("planned");
         const ViewPlan& vp = vpl;
         const bool merge = vp.merge_mask != 0;
         if (merge) {
@@ -2030,6 +2091,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         if (nmax16 == 0) kname = "wide_i64";
         srows = use_pair ? 2 * (uint32_t)pnp : 0;
         if (v == 0) prep = now_ms() - t_prep0;
+        if (v == 0) host_mark("upload issued");
         hipEvent_t ev_k0 = piped ? D.vev[2 * v] : D.ev[0], ev_k1 = piped ? D.vev[2 * v + 1] : D.ev[1];
         // option "timeline": one row per long_kernel lane and pair_kernel group
         uint4* tl = nullptr;
@@ -2391,8 +2453,10 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             // a fused batch's DP time runs from this one launch (not from view
             // 0's start: the host prepared the other views in between)
             if (fused && v + 1 == V) check(op_record(D.vev[2 * V], st, true), "event");
-            if (!fused || v + 1 == V)
+            if (!fused || v + 1 == V) {
                 check(launch_pair(b, pnp, tail_np, nw, (size_t)pair_lds_rows(A) * (lnp + 4) * 4, st), "pair kernel launch");
+                host_mark("pair issued");
+            }
         } else {
             check(use_f16 ? launch_sw_f16(a, np, st) : launch_strip16(a, np, nw, st), "strip kernel launch");
         }
@@ -2678,6 +2742,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         }
         if (trace_on()) fprintf(stderr, "trace: search graph: eligible %d, ops %zu, mode %u\n", (int)use_graph, rec.ops.size(), out.graph);
         const double t_sync0 = now_ms();
+        host_mark("issued");
         // filter_host 3: the filter's own stores, made visible by the end of
         // its dispatch -- an ordinary synchronisation, no copy, no spin
         const bool spin = host_direct && C.filter_host != 3;
@@ -2728,6 +2793,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             upload += u;
         }
         if (trace_on()) fprintf(stderr, "trace: sync-wait %.3f\n", now_ms() - t_sync0);
+        host_mark("synced");
         // exact int64 scores of overflowed lanes: view vv's list and scores
         auto take_wide = [&](size_t vv, uint32_t nov, SearchScores& dst, size_t key_view) {
             const uint32_t* ov = D.d_ovf + (piped ? vv * (ovf_capv + 1) : 0);
@@ -2848,6 +2914,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             take_wide(v, D.h_ovf[0], out, v);
         }
         if (trace_on()) fprintf(stderr, "trace: candidates %.3f (%zu)\n", now_ms() - t_post0, out.cand.size());
+        host_mark("candidates");
         float t;
         if (fused) {
             // one launch for all views: from that launch to the join of the DP

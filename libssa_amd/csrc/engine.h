@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -22,6 +23,8 @@ struct EntryMeta {
     size_t records = 0;             // IDs the plugin handed out
     size_t size() const { return id.size(); }
 };
+
+struct PlanCache;   // engine.cpp: plan_view results of the last queries
 
 struct DeviceDB {
     int device = -1;
@@ -194,6 +197,7 @@ struct DeviceDB {
     PairRows prs[2];
     uint64_t pr_clock = 0;
     size_t rec_begin = 0, rec_end = 0;    // plugin records [rec_begin, rec_end) of this shard
+    std::shared_ptr<PlanCache> plans;
     void release();
 };
 
@@ -263,5 +267,7 @@ ssa_amd_stats_t& stats();
 void dist_overlay_stats(ssa_amd_stats_t* out);   // dist.cpp
 void check(hipError_t e, const char* what);
 double now_ms();
+void host_mark(const char* what);
+std::vector<std::pair<const char*, double>>& host_marks();
 
 }  // namespace ssa

@@ -1757,6 +1757,42 @@ def test_reference_thread_sweep_becomes_device_slot_sweep(tmp_path):
         assert f.read().count("\n") == 36
 
 
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_plan_cache_follows_scoring_and_options(algo, tmp_path):
+    """The per-DB plan cache (engine.cpp cached_plan) reuses a plan only for
+    the same query under unchanged settings: one query searched under
+    BLOSUM62 -11/-1, then gaps -3/-1, then BLOSUM50, then an option change
+    (strip height), then the first setting again -- every full score vector
+    equals the oracle's for the setting in force."""
+    rng = np.random.default_rng(41)
+    lens = np.array([2600] + list(rng.integers(1, 500, 299)), dtype=np.int64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+    q = syn.protein_query(150, 77)
+    codes[int(off[5]) + 2:int(off[5]) + 2 + 150] = q
+    configure(False, ("builtin", "blosum62"), -11, -1)
+    S.init_db(_write_db(str(tmp_path), codes, off))
+    qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+    steps = [("blosum62", -11, -1, None), ("blosum62", -3, -1, None), ("blosum50", -3, -1, None),
+             ("blosum50", -3, -1, 16), ("blosum62", -11, -1, 0)]
+    try:
+        for name, go, ge, pnp in steps:
+            S.init_score_matrix(S.MATRIX_BUILDIN, name)
+            S.init_gap_penalties(go, ge)
+            if pnp is not None:
+                S.set_option("pair_np", pnp)
+            exp = po.scores(algo, q, codes, off, TABLES["matrices"][NAMES.index(name)].copy(), go, ge)
+            for _ in range(2):                   # the second search takes the cached plan
+                sc, ids = _full_scores(qq, algo, len(lens))
+                assert (ids == np.arange(len(lens))).all()
+                assert (sc == exp).all(), (name, go, ge, pnp, np.nonzero(sc != exp)[0][:10])
+            if pnp == 16 and S.stats()["kernel"].startswith("pair"):
+                assert S.stats()["strip_rows"] == 32
+    finally:
+        S.set_option("pair_np", 0)
+
+
 def test_ssa_exit_releases_device_memory(tmp_path):
     """ssa_exit (libssa.c:266-271 frees the reference's state and ends its
     thread pool) also releases the device copies of the DB -- what bench.py's

@@ -166,6 +166,17 @@ run_kgap() (
     python3 "$REPO/tools/api_gap.py" "$OUT" > "$OUT/gap.txt" && head -2 "$OUT/gap.txt"
 )
 
+run_htrace() (
+    # host marks (SSA_AMD_TRACE) over a kernel + copy trace of 30 C2 searches:
+    # tools/host_device_timeline.py.  $1 = name, bench args after it
+    OUT=$(realpath -m gpurun_out/$R/htrace_$1); mkdir -p "$OUT"; shift
+    REPO=$PWD
+    cd /tmp && export TMPDIR=/tmp && export SSA_AMD_TRACE=1
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT" -o run --output-format csv \
+        -- python3 "$REPO/bench.py" --steps 30 --warmup 2 --no-cpu-baseline --no-north-star "$@" > "$OUT/bench.log" 2> "$OUT/trace.log"
+    python3 "$REPO/tools/host_device_timeline.py" "$OUT" "$OUT/trace.log" > "$OUT/timeline.txt" && cat "$OUT/timeline.txt"
+)
+
 run_nsslice() (
     # the north-star N = 8 rank-0 slice on one GPU (the first 1.25 M IDs of
     # the 10 M DB): end to end vs kernel (5 x 20 steps) and the kernel trace's
