@@ -159,6 +159,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *   "long_prio" 1|0      long16 waves at raised issue priority over the pair waves (default 1)
  *   "long_pad" 1|0       long-entry workgroups pad their LDS to the pair kernel's, so a finished one
  *                        leaves a pair workgroup's hole (default 1; 0 measured -6 % on the Swiss-Prot form)
+ *   "filter_onepass" 1|0 the device top-k filter as one launch (a decoupled look-back over its
+ *                        blocks; default 1) or as three (block maxima, prefix, select)
  *   "plan_cache" 1|0     a search with the query and settings of one of the last four reuses
  *                        their plan (residue classes, bounds, strips; default 1); 0: plan each search
  *   "long_gate" 1|0|P    the pair kernel starts after the long-entry workgroups have (default 1;

@@ -60,6 +60,7 @@ struct Config {
     int tail_rows4 = 1;                   // pair kernel tail strips at 4-row granularity (default heights)
     int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
     int long_pad = 1;
+    int filter_onepass = 1;               // kernels.hip filter_onepass (0: three launches)
     int plan_cache = 1;                   // engine.cpp cached_plan (0: plan every search)                     // 1: long-entry workgroups pad their LDS to the pair kernel's (a finished
                                           // one leaves exactly a pair workgroup's hole); 0: their own LDS only
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry

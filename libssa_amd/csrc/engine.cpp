@@ -467,7 +467,7 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
         D.filter_cap = std::max<size_t>(E, 1);
         D.fbuf_bytes = kFilterHeader * 4 + std::max<size_t>(E, 1) * 8;
         D.h_fbuf_regions = 1;
-        dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter summaries");
+        dalloc((void**)&D.d_summary, std::max<size_t>(nb, 1) * kFilterMaxK * 8, "filter summaries");   // (8 B: the one-pass look-back words)
         dalloc((void**)&D.d_before, std::max<size_t>(nb, 1) * kFilterMaxK * 4, "filter scan");
         dalloc((void**)&D.d_thresh_local, std::max<size_t>(nb, 1) * 64 * 4, "filter local thresholds");
         dalloc((void**)&D.d_thresh, std::max<size_t>(nb, 1) * 4, "filter thresholds");
@@ -484,7 +484,10 @@ void upload_pack(DeviceDB& D, HostPack& H, int dev) {
     dalloc((void**)&D.d_flist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
     dalloc((void**)&D.d_frlist, (H.lane_len.size() + 1) * 4, "overflow-flag replay list");
     // overflow counters, then the long-entry dispatch gate (TableArgs::gate)
-    dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe + 16, "overflow counters");
+    // (+ the one-pass filter's ticket and done words, two per query of a
+    // fused batch: zero between searches, FilterArgs::pass)
+    dalloc((void**)&D.d_cnt, 16 * kMaxBatchPipe + 16 + 8 * kMaxFuse, "overflow counters");
+    check(hipMemset(D.d_cnt, 0, 16 * kMaxBatchPipe + 16 + 8 * kMaxFuse), "memset");
     check(hipHostMalloc((void**)&D.h_cnt, 16 * kMaxBatchPipe + 16, hipHostMallocDefault), "pinned");
     const double t_up0 = now_ms();
     if (trace_on()) fprintf(stderr, "trace: pack device allocations %.1f ms\n", t_up0 - t_al0);
@@ -1535,6 +1538,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
     }
     // counters and the long-entry dispatch gate start at 0
     uint32_t* const gate = (uint32_t*)(D.d_cnt + 2 * kMaxBatchPipe);
+    // option "filter_onepass": the filter as one launch (kernels.hip
+    // filter_onepass), its flags told apart from the last pass's by an epoch
+    auto one_pass = [&](FilterArgs& f) {
+        if (!C.filter_onepass) return;
+        f.pass = gate + 4;
+        if (++D.filter_epoch >= 0x20000000u) D.filter_epoch = 1;
+        f.epoch = D.filter_epoch;
+    };
     uint32_t gate_total = 0, gate_base = 0;   // long workgroups launched in all views / before this view
     // (no per-search memset: the gate word only grows, see DeviceDB::gate_count;
     // the counters are zeroed only when this search computes them)
@@ -1627,7 +1638,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             dfree(D.d_fbuf); dfree(D.d_summary); dfree(D.d_before); dfree(D.d_thresh_local); dfree(D.d_thresh);
             check(hipMalloc((void**)&D.d_fbuf, kFilterHeader * 4 + V * E * 8), "filter candidates");
             D.fbuf_bytes = kFilterHeader * 4 + V * E * 8;
-            check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 4), "filter summaries");
+            check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 8), "filter summaries");
             check(hipMalloc((void**)&D.d_before, nb * kFilterMaxK * 4), "filter scan");
             check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
             check(hipMalloc((void**)&D.d_thresh, nb * 4), "filter thresholds");
@@ -1737,7 +1748,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const size_t nb = V * ((E + kFilterBlock - 1) / kFilterBlock);
                 if (D.filter_blocks_cap < nb) {
                     dfree(D.d_summary); dfree(D.d_before); dfree(D.d_thresh_local); dfree(D.d_thresh);
-                    check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 4), "filter summaries");
+                    check(hipMalloc((void**)&D.d_summary, nb * kFilterMaxK * 8), "filter summaries");
                     check(hipMalloc((void**)&D.d_before, nb * kFilterMaxK * 4), "filter scan");
                     check(hipMalloc((void**)&D.d_thresh_local, nb * 64 * 4), "filter local thresholds");
                     check(hipMalloc((void**)&D.d_thresh, nb * 4), "filter thresholds");
@@ -2591,6 +2602,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.counters = reg;
                 f.status = gate + 2;
                 f.cand = (uint2*)(reg + kFilterHeader);
+                one_pass(f);
                 check(launch_filter(f, st), "filter launch");
                 check(op_copy((uint8_t*)D.h_fbuf + v * hreg, reg, kFilterHeader * 4 + 8 * std::min(D.h_cand_cap, E),
                                      hipMemcpyDeviceToHost, st), "D2H candidates");
@@ -2625,6 +2637,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             f.q_scores = E;
             f.q_ovf = ovf_capv + 1;
             f.q_counters = dreg / 4;
+            one_pass(f);
             check(launch_filter(f, st), "filter launch");
             for (size_t vv = 0; vv < V; vv++)
                 check(op_copy((uint8_t*)D.h_fbuf + vv * hreg, (uint8_t*)D.d_fbuf + vv * dreg,
@@ -2671,6 +2684,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 f.exact_lanes = D.d_exact;
                 f.exact_lane0 = long_groups * 64;
             }
+            one_pass(f);
             check(launch_filter(f, st), "filter launch");
             // (the stream's end, and so the host's wake-up, covers the tier)
             if (side_tier) check(op_wait(st, D.ev[8]), "event wait");

@@ -153,6 +153,7 @@ struct DeviceDB {
     uint32_t tier_hint = 0;
     bool cnt_dirty = true;
     uint32_t filter_seq = 0;              // the last FilterArgs::host_seq (never 0)
+    uint32_t filter_epoch = 0;            // the last FilterArgs::epoch (one-pass filter)
     uint32_t* d_smax = nullptr;
     size_t smax_cap = 0;
     uint4* d_rowbuf2 = nullptr;           // part 1's row buffer (StripArgs::rowbuf2), as d_rowbuf

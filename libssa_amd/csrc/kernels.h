@@ -262,6 +262,17 @@ struct FilterArgs {
     const uint2* entry_lane;
     uint32_t* exact_lanes;
     uint32_t exact_lane0;      // lanes below it (the long-entry kernels') are scored exactly anyway
+    // one pass (filter_onepass): the three steps in one launch.  Blocks take
+    // their block index from a start-order ticket (pass[2q]) and chain the
+    // prefix by a decoupled look-back through summary, read as 8-byte words
+    // [nq][nblocks][kFilterMaxK] (the allocation is sized for them): per lane
+    // (1 << 31 | epoch << 2 | 1 aggregate / 2 inclusive) << 32 | list element
+    // (epoch < 2^29) -- stale
+    // epochs read as not ready, so nothing is cleared between searches; the
+    // last block to finish (pass[2q + 1]) resets both pass words.  pass
+    // null: the three launches.
+    uint32_t* pass;
+    uint32_t epoch;
 };
 constexpr int kFilterSeqWord = 15;    // header word that carries FilterArgs::host_seq
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

@@ -757,6 +757,7 @@ void set_filter_prefix_regs(int on) { g_prefix_regs = on; }
 // kSelectPer consecutive entries per thread (one mini, so one bound), a
 // quarter of the workgroups of one entry per thread
 constexpr uint32_t kSelectPer = 4;
+__device__ void filter_to_host(const FilterArgs& a);
 __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     const FilterArgs a = filter_query(a0);
     const uint32_t tid = blockIdx.x * 256 + threadIdx.x;
@@ -796,6 +797,12 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     }
     __syncthreads();
     if (!last) return;
+    filter_to_host(a);
+}
+
+// The result into pinned host memory (FilterArgs::host_out), by the last
+// block of the filter pass to finish; resets *a.done for the next search.
+__device__ void filter_to_host(const FilterArgs& a) {
     __threadfence();                           // every block's candidates visible here
     const uint32_t nc = __hip_atomic_load(&a.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto put = [&](uint32_t* p, uint32_t v) {
@@ -827,9 +834,174 @@ __global__ void __launch_bounds__(256) filter_select(const FilterArgs a0) {
     }
 }
 
+// One pass (FilterArgs::pass): filter_block, filter_prefix and
+// filter_select as one launch -- no kernel boundaries on the path from the DP
+// kernels to the result, and the scores are read once.  A block takes its
+// block index b from a start-order ticket, so every block it waits for has
+// started; wave 0 computes the block's list of mini maxima (as filter_block),
+// publishes it (aggregate), and walks back over the blocks before it --
+// merging aggregates until it meets an inclusive prefix -- to the exclusive
+// prefix whose K-th largest is T_block[b] (filter_prefix's value), then
+// publishes its own inclusive prefix over the aggregate.  Each lane's list
+// element travels with its state in one 8-byte word ((1 << 31 | epoch << 2 |
+// state) << 32 | value; state 1 aggregate, 2 inclusive), written and read at device
+// scope (write-through / past the XCD's L2: the XCDs' L2s are not coherent),
+// so a list is ready when all 64 lanes show this pass's epoch and one state
+// -- no separate flag, one round trip per look -- and the walk reads eight
+// predecessors per round trip.  Then every thread tests the entries it
+// loaded (filter_select).
+template <int KW>
+__device__ int32_t filter_lookback(uint64_t* lb, uint32_t ep, uint32_t b, int32_t mine, int lane, int K) {
+    auto put = [&](uint32_t state, int32_t v) {
+        const uint64_t w = (uint64_t)(0x80000000u | ep << 2 | state) << 32 | (uint32_t)v;
+        __hip_atomic_store(lb + (size_t)b * kFilterMaxK + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (b == 0) {
+        put(2u, mine);
+        return INT32_MIN;
+    }
+    put(1u, mine);
+    constexpr int W = 8;                       // predecessors per round trip
+    int32_t excl = INT32_MIN;
+    int32_t j = (int32_t)b - 1;                // (block 0 always publishes an inclusive prefix)
+    for (;;) {
+        uint64_t w[W];
+#pragma unroll
+        for (int i = 0; i < W; i++)
+            w[i] = j - i >= 0 ? __hip_atomic_load(lb + (size_t)(j - i) * kFilterMaxK + lane, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0ull;
+        int used = 0;
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            if (j - i < 0) break;
+            const uint32_t hi = (uint32_t)(w[i] >> 32);
+            // (bit 31 set: no pair of int32 scores an earlier three-launch
+            // pass left in these words looks like a state word)
+            const bool cur = hi >> 31 && ((hi >> 2) & 0x1fffffffu) == ep;
+            const uint64_t agg = __ballot(cur && (hi & 3u) == 1u), inc = __ballot(cur && (hi & 3u) == 2u);
+            if (agg != ~0ull && inc != ~0ull) break;     // not published yet (or changing state): look again
+            excl = merge_topk_w<KW>(excl, (int32_t)(uint32_t)w[i], lane, K);
+            used = i + 1;
+            if (inc == ~0ull) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        j -= used;
+        if (used == 0) __builtin_amdgcn_s_sleep(1);
+    }
+    put(2u, merge_topk_w<KW>(excl, mine, lane, K));
+    return excl;
+}
+
+template <int KW>
+__global__ void __launch_bounds__(256) filter_onepass(const FilterArgs a0) {
+    FilterArgs a = filter_query(a0);
+    uint32_t* const pass = a0.pass + 2 * blockIdx.y;       // [0] ticket, [1] blocks done
+    __shared__ int32_t mini_max[kMinisPerBlock];
+    __shared__ int32_t tloc[kMinisPerBlock];
+    __shared__ uint32_t sb;
+    __shared__ int32_t tblock;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) sb = atomicAdd(pass, 1u);
+    __syncthreads();
+    const uint32_t b = sb;
+    const uint32_t base = b * kFilterBlock;
+    constexpr int MW = kMinisPerBlock / 4;
+    int32_t x[MW];
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        const uint32_t e = base + (i * 4 + wave) * kMini + lane;
+        x[i] = e < a.n ? a.scores[a.order ? a.order[e] : e] : INT32_MIN;
+    }
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        const uint32_t e = base + (i * 4 + wave) * kMini + lane;
+        int32_t y = x[i];
+        // an upper bound (rare-code merge) is no lower bound of the heap root
+        if (a.emask && e < a.n && (a.emask[e] & a.merge_mask) && a.entry_lane[e].y >= a.exact_lane0) y = INT32_MIN;
+        const int32_t mx = wave_max(y, lane);
+        if (lane == 0) mini_max[i * 4 + wave] = mx;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int K = (int)a.k;
+        const int32_t mine = mini_max[lane];
+        int32_t run = INT32_MIN, tl = INT32_MIN;
+        int m0 = 0;
+        if (b == 0) {
+            // the DB's first mini seeds the list with its K largest entries
+            // (filter_block); its upper-bound entries are left out as above
+            int32_t y = x[0];
+            if (a.emask && (uint32_t)lane < a.n && (a.emask[lane] & a.merge_mask) && a.entry_lane[lane].y >= a.exact_lane0)
+                y = INT32_MIN;
+            const int32_t srt = sort_desc64(y, lane);
+            run = lane < K ? srt : INT32_MIN;
+            m0 = 1;
+        }
+        for (int m = m0; m < kMinisPerBlock; m++) {
+            const int32_t t = __builtin_amdgcn_readlane(run, K - 1);
+            tl = lane == m ? t : tl;
+            run = insert_desc(run, __builtin_amdgcn_readlane(mine, m), lane, K);
+        }
+        tloc[lane] = tl;
+        // (this query's look-back words: FilterArgs::summary read as 8-byte words)
+        uint64_t* lb = (uint64_t*)a0.summary + (size_t)blockIdx.y * a0.nblocks * kFilterMaxK;
+        const int32_t excl = filter_lookback<KW>(lb, a0.epoch & 0x1fffffffu, b, lane < K ? run : INT32_MIN, lane, K);
+        if (lane == 0) tblock = __builtin_amdgcn_readlane(excl, K - 1);
+    }
+    __syncthreads();
+    const int32_t T = tblock;
+    if (b == 0) {
+        for (uint32_t v = threadIdx.x; v < a.nviews; v += 256) a.counters[3 + v] = a.ovf_count[(size_t)v * a.ovf_stride];
+        if (threadIdx.x == 0 && a.status) a.counters[2] = *a.status;
+    }
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        const uint32_t e = base + (i * 4 + wave) * kMini + lane;
+        const int32_t t = max(T, tloc[i * 4 + wave]);
+        if (e < a.n && (x[i] == INT32_MIN || x[i] > t)) {
+            const uint32_t c = atomicAdd(&a.counters[0], 1u);
+            a.cand[c] = make_uint2(e, (uint32_t)x[i]);
+            if (a.emask && (a.emask[e] & a.merge_mask)) {
+                const uint32_t l = a.entry_lane[e].y;
+                if (l >= a.exact_lane0) a.exact_lanes[atomicAdd(&a.counters[1], 1u)] = l;
+            }
+        }
+    }
+    // the last block to finish resets the pass words (and hands the result
+    // to the host when asked)
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // (this block's candidates, device-wide, only when the last block
+        // reads them: the fence writes back the XCD's L2)
+        if (a.host_out) __threadfence();
+        last = atomicAdd(pass + 1, 1u) == gridDim.x - 1 ? 1u : 0u;
+        if (last) {
+            __hip_atomic_store(pass, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(pass + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!last || !a.host_out) return;
+    a.done = pass + 1;                         // (filter_to_host clears it again: already 0)
+    filter_to_host(a);
+}
+
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
     const uint32_t nq = a.nq > 1 ? a.nq : 1u;
+    if (a.pass) {
+        if (a.host_out && nq > 1) return hipErrorInvalidValue;
+        if (a.k <= 16) (void)ssa_launch((const void*)&filter_onepass<16>, dim3(a.nblocks, nq), dim3(256), 0, st, a);
+        else if (a.k <= 32) (void)ssa_launch((const void*)&filter_onepass<32>, dim3(a.nblocks, nq), dim3(256), 0, st, a);
+        else (void)ssa_launch((const void*)&filter_onepass<64>, dim3(a.nblocks, nq), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     (void)ssa_launch((const void*)&filter_block, dim3(a.nblocks, nq), dim3(256), 0, st, a);
     if (g_prefix_regs && a.nblocks <= (uint32_t)(kPrefixWaves * kPrefixRegs)) {
         if (a.k <= 16) (void)ssa_launch((const void*)&filter_prefix_r<16>, dim3(1, nq), dim3(64 * kPrefixWaves), 0, st, a);

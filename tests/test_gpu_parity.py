@@ -1236,25 +1236,31 @@ def test_device_filter_candidate_count_is_exact(n, pattern):
             # option filter_host: the result written into pinned host memory
             # by the last filter block (with a system-scope release, or with
             # system-scope stores) instead of the D2H copy -- incl. more
-            # candidates than the pinned buffer holds ("rising")
-            for fh in (0, 1, 2, 3):
-                S.set_option("filter_host", fh)
-                for k in (1, 10, 64):
-                    got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
-                    assert got == po.topk(exp, ids, k), (pattern, k, fh)
-                    assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, fh)
+            # candidates than the pinned buffer holds ("rising"); the filter
+            # as one launch (decoupled look-back, the default) and as three
+            for one in (1, 0):
+                S.set_option("filter_onepass", one)
+                for fh in (0, 1, 2, 3):
+                    S.set_option("filter_host", fh)
+                    for k in (1, 10, 64):
+                        got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
+                        assert got == po.topk(exp, ids, k), (pattern, k, fh, one)
+                        assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, fh, one)
             # the block scan at every list width (filter_prefix_r<16/32/64>,
-            # k on both sides of 16 and 32) and the general scan
+            # k on both sides of 16 and 32) and the general scan; the
+            # one-pass look-back's merges at every width
             S.set_option("filter_host", 0)
-            for regs in (1, 0):
+            for one, regs in ((0, 1), (0, 0), (1, 1)):
+                S.set_option("filter_onepass", one)
                 S.set_option("filter_prefix_regs", regs)
                 for k in (1, 10, 16, 17, 32, 33, 64):
                     got = [(h["score"], h["id"]) for h in S.sw_align(qq, k, 16)]
-                    assert got == po.topk(exp, ids, k), (pattern, k, regs)
-                    assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, regs)
+                    assert got == po.topk(exp, ids, k), (pattern, k, regs, one)
+                    assert S.stats()["filter_candidates"] == _filter_candidates(exp, k), (pattern, k, regs, one)
         finally:
             S.set_option("filter_host", 0)
             S.set_option("filter_prefix_regs", 1)
+            S.set_option("filter_onepass", 1)
         S.free_sequence(qq)
 
 
@@ -1326,11 +1332,16 @@ def test_multiview_device_filter_matches_full_scan(mode):
                                         np.int64)
                     assert len(order_sc) == total
                     for k in (1, 10, 64):
-                        fn(qq, k, 16)
-                        assert S.stats()["filter_candidates"] == _filter_candidates(order_sc, k), (mode, chunk, k)
+                        for one in (1, 0):            # the filter as one launch and as three
+                            S.set_option("filter_onepass", one)
+                            fn(qq, k, 16)
+                            assert S.stats()["filter_candidates"] == _filter_candidates(order_sc, k), \
+                                (mode, chunk, k, one)
+                        S.set_option("filter_onepass", 1)
                 S.free_sequence(qq)
     finally:
         S.set_option("no_filter", 0)
+        S.set_option("filter_onepass", 1)
         S.set_chunk_size(1000)
         S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 1, 1)
 
@@ -1624,6 +1635,10 @@ def test_search_batch_fused_launch(algo):
                     S.set_option("batch_fuse", 1)
                     got = S.search_batch(qs, algo, k)
                     assert got == exp, (qlens, opts, k)
+                    # (the three-launch filter over the fused batch's queries)
+                    S.set_option("filter_onepass", 0)
+                    assert S.search_batch(qs, algo, k) == exp, (qlens, opts, k, "three-launch filter")
+                    S.set_option("filter_onepass", 1)
                     # every query's own filter pass: the same candidates as alone
                     assert S.stats()["filter_candidates"] == ncand, (qlens, opts, k)
                     # NW with long_kernel groups and counters keeps one launch per query
@@ -1637,6 +1652,7 @@ def test_search_batch_fused_launch(algo):
             S.set_option("batch_fuse", 1)
             S.set_option("pair_parts", 0)
             S.set_option("long_groups", -1)
+            S.set_option("filter_onepass", 1)
     assert lens.max() > 0
 
 
