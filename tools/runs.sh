@@ -198,6 +198,21 @@ print("nsslice median end-to-end", st.median(v), "kernel", st.median(k), "gap %"
 PYEOF
 )
 
+run_refresh_pmc() (
+    # this build's PMC figures for the bench lines' roofline (profiles/
+    # traffic.json, keyed by workload and kernel-source hash): stats / fetch /
+    # write / valu / lds passes of C2 and the north-star shard, filed under
+    # $PDIR/pmc2 (default profiles/r06; copied back from gpurun_out by the
+    # caller as well, with the same command)
+    for cfg in "c2:--config c2" "north_star:--config north_star"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        PASSES="stats fetch write valu lds" bash tools/profile_pmc.sh gpurun_out/$R/pmc2/$name $args || exit 1
+        P=${PDIR:-profiles/r06}/pmc2
+        mkdir -p $P && rm -rf $P/$name && cp -r gpurun_out/$R/pmc2/$name $P/ || exit 1
+        python3 tools/traffic_from_pmc.py $P/$name || exit 1
+    done
+)
+
 run_final() (
     # the default bench line (python bench.py: C2 headline, north_star,
     # cpu_baseline) under rocprofv3 --kernel-trace --stats: the summary whose
