@@ -36,8 +36,10 @@ def split(d):
                 if key in e[2] and e[0] >= after:
                     return e
             return None
-        fb = first("filter_block")
-        fs = first("filter_select")
+        # (the filter's first and last kernels: filter_block .. filter_select,
+        # or the one launch filter_onepass)
+        fb = first("filter_block") or first("filter_onepass")
+        fs = first("filter_select") or first("filter_onepass")
         cp = first("copyBuffer", fs[1] if fs else 0) or first("copy", fs[1] if fs else 0)
         up = first("upload_kernel", cp[1] if cp else 0)
         tb = first("pair_tables_kernel", up[1] if up else 0)
