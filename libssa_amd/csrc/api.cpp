@@ -382,7 +382,7 @@ p_alignment_list align(p_query q, size_t k, int bw, int at, int algo) {
     // call's return -- the caller's own time -- to this one's)
     static double last_return = 0;
     if (trace_on()) {
-        host_marks().clear();
+        host_marks_begin(true);
         host_mark("entry");
     }
     test_configuration(q);
@@ -398,6 +398,7 @@ p_alignment_list align(p_query q, size_t k, int bw, int at, int algo) {
         for (size_t i = 1; i < m.size(); i++) fprintf(stderr, ", %s %.1f", m[i].first, (m[i].second - t0) * 1e3);
         fprintf(stderr, "\n");
         last_return = now_ms();
+        host_marks_begin(false);
     }
     return L;
 }

@@ -31,14 +31,20 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// SSA_AMD_TRACE: the host's timeline of one search (host_mark at the points
-// below, printed by api.cpp run_search relative to its entry)
-std::vector<std::pair<const char*, double>>& host_marks() {
-    thread_local std::vector<std::pair<const char*, double>> m;
-    return m;
+// SSA_AMD_TRACE: the host's timeline of one call (host_mark at the points
+// below), recorded on the calling thread between host_marks_begin and the
+// print in api.cpp align(); other threads (device slots) record nothing
+namespace {
+thread_local std::vector<std::pair<const char*, double>> t_marks;
+thread_local bool t_marks_on = false;
+}  // namespace
+const std::vector<std::pair<const char*, double>>& host_marks() { return t_marks; }
+void host_marks_begin(bool on) {
+    t_marks.clear();
+    t_marks_on = on;
 }
 void host_mark(const char* what) {
-    if (trace_on()) host_marks().emplace_back(what, now_ms());
+    if (t_marks_on) t_marks.emplace_back(what, now_ms());
 }
 
 void check(hipError_t e, const char* what) {

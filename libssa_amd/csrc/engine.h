@@ -269,6 +269,7 @@ void dist_overlay_stats(ssa_amd_stats_t* out);   // dist.cpp
 void check(hipError_t e, const char* what);
 double now_ms();
 void host_mark(const char* what);
-std::vector<std::pair<const char*, double>>& host_marks();
+void host_marks_begin(bool on);
+const std::vector<std::pair<const char*, double>>& host_marks();
 
 }  // namespace ssa
