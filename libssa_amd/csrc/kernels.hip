@@ -864,6 +864,13 @@ __device__ int32_t filter_lookback(uint64_t* lb, uint32_t ep, uint32_t b, int32_
     constexpr int W = 8;                       // predecessors per round trip
     int32_t excl = INT32_MIN;
     int32_t j = (int32_t)b - 1;                // (block 0 always publishes an inclusive prefix)
+    // A bounded wait: every predecessor has started (tickets) and publishes
+    // without waiting on later blocks, so the walk ends; should one never
+    // publish (a faulted wave), the walk stops after 20 ms with the lists it
+    // has merged -- the k-th largest of a subset of the earlier minis is still
+    // a lower bound of the heap root, so the filter forwards more entries and
+    // the result stays exact.
+    const uint64_t t_wait0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         uint64_t w[W];
 #pragma unroll
@@ -891,7 +898,10 @@ __device__ int32_t filter_lookback(uint64_t* lb, uint32_t ep, uint32_t b, int32_
         }
         if (done) break;
         j -= used;
-        if (used == 0) __builtin_amdgcn_s_sleep(1);
+        if (used == 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t_wait0 > 2000000u) break;   // 20 ms at 100 MHz
+            __builtin_amdgcn_s_sleep(1);
+        }
     }
     put(2u, merge_topk_w<KW>(excl, mine, lane, K));
     return excl;
