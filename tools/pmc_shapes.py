@@ -66,7 +66,9 @@ for d in sys.argv[1:]:
     ldsa = mean([x["SQ_LDS_IDX_ACTIVE"] / x["SQ_INSTS_LDS"] for x in lv]) if lv else float("nan")
     # wave-instructions per SIMD and cycle at that clock
     ipc = pair_valu / 1024 / (clk * dur_ns) if dur_ns else float("nan")
-    print(f"{name:10s} pair {dur_ns / 1e6:7.3f} ms  clock {clk:5.3f} GHz  "
+    # (cycles, not milliseconds, compare passes: the chip's clock under load
+    # differs from pass to pass -- MI355X_MICROARCH.md 'DVFS give-back')
+    print(f"{name:10s} pair {dur_ns / 1e6:7.3f} ms  clock {clk:5.3f} GHz  Mcycles {dur_ns * clk / 1e6:6.2f}  "
           f"VALU/cell pair {pair_valu * 64 / cells:5.3f} all-DP {dp_valu * 64 / cells:5.3f}  "
           f"cycles/VALU-instr per SIMD {1 / ipc:5.2f}  LDS conflict cyc/instr {conf:5.2f}  "
           f"LDS active cyc/instr {ldsa:5.2f}  busy {busy:4.2f}  kernel TCUPS {b['kernel']['kernel_gcups'] / 1e3:6.2f}")
