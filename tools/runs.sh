@@ -213,6 +213,29 @@ run_refresh_pmc() (
     done
 )
 
+run_nwshapes() (
+    # NW on the reference's shape and the Swiss-Prot form (with and without
+    # its tail, with the rare-code merge): per-kernel time under rocprofv3
+    # --kernel-trace --stats
+    for cfg in "ref_nw:--config ref --algo nw" "sprot_nw:--config sprot --algo nw" \
+               "sprot_nw_notail:--config sprot --algo nw --long-tail 0" \
+               "sprot_nw_merge:--config sprot --algo nw --option rare_merge=1"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        OUT=$(realpath -m gpurun_out/$R/nwshapes/$name); mkdir -p "$OUT"
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv \
+            -- python3 "$OLDPWD/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-north-star $args > "$OUT/bench.json" 2> "$OUT/bench.err" ) || exit 1
+        python3 - "$OUT" <<'PYEOF'
+import csv, glob, json, sys
+d = sys.argv[1]
+b = json.loads(open(d + "/bench.json").read().strip().splitlines()[-1])
+print(d.rsplit("/", 1)[1], b["value"], b["kernel"]["kernel_gcups"], b["kernel"]["name"], b["kernel"].get("strip_rows"), b.get("topk_vs_reference"))
+for r in csv.DictReader(open(glob.glob(d + "/**/*kernel_stats.csv", recursive=True)[0])):
+    if float(r["Percentage"]) > 0.5:
+        print("   ", r["Name"][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us", r["Percentage"])
+PYEOF
+    done
+)
+
 run_final() (
     # the default bench line (python bench.py: C2 headline, north_star,
     # cpu_baseline) under rocprofv3 --kernel-trace --stats: the summary whose
