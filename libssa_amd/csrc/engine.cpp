@@ -2306,6 +2306,9 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 if (C.long_gate > 1 && C.long_gate < 100) want = std::max<uint32_t>(1, want * (uint32_t)C.long_gate / 100);
                 ta.gate = gate;
                 ta.gate_target = gate0 + gate_base + want;
+                if (trace_on() && v == 0)
+                    fprintf(stderr, "trace: long gate: groups %u (4-wave %u), workgroups %u, resident %u, want %u, lds %zu\n",
+                            long_groups, long4, gate_total - gate_base, resident, want, lds_long);
             }
             check(launch_pair_tables(ta, st), "pair tables kernel");
         } else {

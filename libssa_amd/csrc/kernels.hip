@@ -1624,7 +1624,18 @@ static hipError_t launch_long_k(const LongArgs& a, hipStream_t st) {
     constexpr size_t kDynMax = kPairLdsMax - 8192;
     const size_t need = long_lds_bytes(a.alpha, W, RL);
     if (need > kDynMax) return hipErrorInvalidValue;
-    const size_t bytes = std::max<size_t>(need, std::min<size_t>(a.lds_min, kDynMax));
+    // the padding (LongArgs::lds_min) is the pair workgroup's whole footprint:
+    // the kernel's static LDS (W = 4: the 6 KiB ring) counts against it, or a
+    // W = 4 workgroup outgrows a pair workgroup's hole -- one per CU instead
+    // of two, and the tables kernel's gate, sized for two, waits for
+    // workgroups that cannot start (NW on the Swiss-Prot form: 2.6 ms a search)
+    static const size_t static_lds = [] {
+        hipFuncAttributes fa{};
+        return hipFuncGetAttributes(&fa, (const void*)long_kernel<W, RL, NW, TRK>) == hipSuccess ? fa.sharedSizeBytes
+                                                                                                  : 0;
+    }();
+    const size_t pad = std::min<size_t>(a.lds_min, kDynMax);
+    const size_t bytes = std::max<size_t>(need, pad > static_lds ? pad - static_lds : 0);
     const hipError_t e = lds_attr_once((const void*)long_kernel<W, RL, NW, TRK>, attr, (int)kDynMax);
     if (e != hipSuccess) return e;
     constexpr int EPW = kLongWaves / W;
