@@ -236,6 +236,27 @@ PYEOF
     done
 )
 
+run_kshapes() (
+    # per-kernel time of any bench shapes under rocprofv3 --kernel-trace
+    # --stats: SHAPES="name:bench args;name2:args2"
+    IFS=';' read -ra CFGS <<< "$SHAPES"
+    for cfg in "${CFGS[@]}"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        OUT=$(realpath -m gpurun_out/$R/kshapes/$name); mkdir -p "$OUT"
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv \
+            -- python3 "$OLDPWD/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-north-star $args > "$OUT/bench.json" 2> "$OUT/bench.err" ) || exit 1
+        python3 - "$OUT" <<'PYEOF'
+import csv, glob, json, sys
+d = sys.argv[1]
+b = json.loads(open(d + "/bench.json").read().strip().splitlines()[-1])
+print(d.rsplit("/", 1)[1], b["value"], b["kernel"]["kernel_gcups"], b["kernel"]["name"], b.get("topk_vs_reference"))
+for r in csv.DictReader(open(glob.glob(d + "/**/*kernel_stats.csv", recursive=True)[0])):
+    if float(r["Percentage"]) > 1.0:
+        print("   ", r["Name"][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us", r["Percentage"])
+PYEOF
+    done
+)
+
 run_final() (
     # the default bench line (python bench.py: C2 headline, north_star,
     # cpu_baseline) under rocprofv3 --kernel-trace --stats: the summary whose
