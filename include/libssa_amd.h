@@ -136,7 +136,8 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        them): auto (4 for groups beyond "long4_share_pct", 1
  *                        for the rest), always 4, always 1
  *   "long4_share_pct" P  auto: 4 waves per entry for groups longer than P % of
- *                        one SIMD's share of all columns
+ *                        one SIMD's share of all columns (default 1500: where one
+ *                        wave's latency would outlast the pair kernel)
  *   "long16" 1|0         SW long entries on packed 16-bit patterns, one wave
  *                        per entry, whenever min(m, n) x max score fits (default);
  *                        0: the int32 kernel ("long_waves" applies to it)

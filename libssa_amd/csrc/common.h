@@ -47,7 +47,8 @@ struct Config {
     int long_groups = -1;                 // leading groups scored by long_kernel: -1 auto, 0 never, N forced
     int long_share_pct = 50;              // auto: groups longer than this % of a SIMD's share of all columns
     int long_waves = 0;                   // waves per long entry: 0 auto, 4 (rows over a workgroup) or 1
-    int long4_share_pct = 400;            // auto: 4 waves for groups longer than this % of a SIMD's share
+    int long4_share_pct = 1500;           // auto: 4 waves for groups longer than this % of a SIMD's share
+                                          // (400 until round 6: NW's Swiss-Prot form +11 % at 1500, engine.cpp)
     int long16 = 1;                       // SW long entries on packed 16-bit patterns (long16_kernel) when exact
     int graph = 0;                        // 1: the usual single-view search runs as cached HIP graphs (engine.cpp
                                           // run_ops; measured slower than the direct calls on ROCm 7.2,

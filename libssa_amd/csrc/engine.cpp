@@ -941,6 +941,7 @@ static int long16_rl(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t
     return 16;
 }
 
+constexpr double kLongTypical = 4.0;   // long_plan: the length tail's multiple of the median group
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
                           uint32_t scale = 1) {
     const Config& C = cfg();
@@ -953,13 +954,23 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
     uint32_t g = 0;
     if (C.long_groups > 0) {
         g = std::min<uint32_t>((uint32_t)C.long_groups, D.ngroups);
-    } else if (D.ngroups >= 2 * D.nsimd) {
-        // (a smaller DB does not fill the chip twice over: every wave starts
-        // at once and no group outlasts a drained chip)
+    } else {
+        // A group is routed when its pair-kernel wave -- one lane per entry,
+        // every column of its longest entry, strip after strip -- would
+        // outlast the launch: on a DB that fills the chip twice over, when it
+        // is longer than long_share_pct % of one SIMD's share of all columns
         // (a lower threshold costs more than it gains: long_kernel's cost per
         // cell is several times pair_kernel's -- the 548 k-entry DB: 40 %
-        // 9.7, 50 % 10.9, 65 % 10.9 TCUPS)
-        const double thr = (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0 * scale;
+        // 9.7, 50 % 10.9, 65 % 10.9 TCUPS); and on any DB never unless it is
+        // kLongTypical times the median group's length -- a length tail (UniProt's
+        // 5-35 k-residue entries) then goes to the long kernels even when the
+        // DB is too small for the share rule (a 30 k-entry DB with such a tail
+        // ran 48 ms in one pair wave), while a DB without a tail keeps its
+        // groups (a moderate DB's share is shorter than its typical group:
+        // the share rule alone routed half of a 150 k-entry DB's groups)
+        double thr = kLongTypical * (double)D.group_ncols[D.ngroups / 2];
+        if (D.ngroups >= 2 * D.nsimd)
+            thr = std::max(thr, (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0 * scale);
         while (g < D.ngroups && g < kLongMaxGroups && D.group_ncols[g] > thr) g++;
     }
     g = std::max(g, need);
@@ -2155,6 +2166,14 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             } else if (C.long_waves == 4) {
                 long4 = long_groups;
             } else if (C.long_waves == 0) {
+                // (the 4-wave kernel cuts an entry's latency ~3x at more total
+                // issue: worth it only where one wave would outlast the pair
+                // kernel -- an entry's one-wave time per column and query row
+                // against the pair kernel's per column and strip makes that
+                // ~15x a SIMD's share for q = 513 (NW's Swiss-Prot form: one
+                // wave 12.7 against four 11.4 TCUPS at its 11.7x; a 30 k- or
+                // 150 k-entry DB with that tail, 140x / 39x: four waves ahead,
+                // profiles/r06/kshapes))
                 const double thr4 = (double)D.ncols_sum / D.nsimd * C.long4_share_pct / 100.0;
                 while (long4 < long_groups && D.group_ncols[long4] > thr4) long4++;
             }

@@ -318,7 +318,7 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0, kerne
             S.set_option("long_groups", -1)
             S.set_option("long_waves", 0)
             S.set_option("long16", 1)
-            S.set_option("long4_share_pct", 400)
+            S.set_option("long4_share_pct", 1500)   # (the default)
         S.free_sequence(qq)
 
 
