@@ -855,9 +855,38 @@ static uint32_t strip_parts(uint32_t T) {
 }
 
 // long_kernel at 4 waves per entry: rows per lane for an m-row query
-static int long_rl4(size_t m) { return m <= 512 ? 2 : m <= 768 ? 3 : 4; }
+// The rows per lane of a long-entry pass: the instantiated RL whose passes
+// over the query cost the fewest row steps per column, ceil(m / (lanes RL))
+// (RL + 1) (ties: the larger RL, fewer passes) -- an entry's latency is that times
+// its columns, and the longest entries' latency is the long kernels'
+// critical path (until round 6 the plan took the smallest single-pass RL of
+// 4, 8, 9, 12, 16, else 16: q = 1046 ran two 16-row passes, 32 row steps,
+// where two 9-row passes take 18 -- NW on the Swiss-Prot form 10.5 against
+// 13.3 TCUPS beside it -- and q = 287 one 8-row pass where 5 rows do)
+template <size_t N>
+static int long_rl_fewest(size_t m, size_t lanes, const int (&rls)[N]) {
+    int best = rls[0];
+    size_t best_cost = SIZE_MAX;
+    for (int rl : rls) {
+        // (+1 row step per pass: its ramp, boundary row and profile)
+        const size_t cost = (m + lanes * rl - 1) / (lanes * rl) * (rl + 1);
+        if (cost <= best_cost) {
+            best_cost = cost;
+            best = rl;
+        }
+    }
+    return best;
+}
+// ... at four waves per entry (its rows over the workgroup: 256 RL rows a pass)
+static int long_rl4(size_t m) {
+    static constexpr int kRl[] = {2, 3, 4};
+    return long_rl_fewest(std::max<size_t>(m, 1), 256, kRl);
+}
 // ... at one wave per entry
-static int long_rl1(size_t m) { return m <= 256 ? 4 : m <= 512 ? 8 : m <= 576 ? 9 : m <= 768 ? 12 : 16; }
+static int long_rl1(size_t m) {
+    static constexpr int kRl[] = {4, 5, 6, 7, 8, 9, 12, 16};   // (kernels.hip launch_long)
+    return long_rl_fewest(std::max<size_t>(m, 1), 64, kRl);
+}
 
 // The exact int32 re-score tier (kernels.h LongArgs::list): the DP kernels'
 // overflowed lanes are re-scored by long_kernel (one wave per entry, the

@@ -1669,6 +1669,11 @@ hipError_t launch_long(const LongArgs& a, int w, int rl, bool nw, hipStream_t st
     if (w != 1) return hipErrorInvalidValue;
     switch (rl) {
         case 4: return nw ? launch_long_t<1, 4, true>(a, st) : launch_long_t<1, 4, false>(a, st);
+        // (5-7: queries of 257-448 rows in one pass without RL 8's idle rows,
+        // engine.cpp long_rl1)
+        case 5: return nw ? launch_long_t<1, 5, true>(a, st) : launch_long_t<1, 5, false>(a, st);
+        case 6: return nw ? launch_long_t<1, 6, true>(a, st) : launch_long_t<1, 6, false>(a, st);
+        case 7: return nw ? launch_long_t<1, 7, true>(a, st) : launch_long_t<1, 7, false>(a, st);
         case 8: return nw ? launch_long_t<1, 8, true>(a, st) : launch_long_t<1, 8, false>(a, st);
         case 9: return nw ? launch_long_t<1, 9, true>(a, st) : launch_long_t<1, 9, false>(a, st);
         case 12: return nw ? launch_long_t<1, 12, true>(a, st) : launch_long_t<1, 12, false>(a, st);

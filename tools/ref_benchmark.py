@@ -13,7 +13,10 @@ residues; no network for UniProt) stands in, and data/P18080 is the query
 file the reference ships (tests/golden/data/P18080.fasta).
 
 usage (on the GPU box, after make -C oracle ref):
-    python tools/ref_benchmark.py <out dir> [SSA_AMD_DEVICES value]
+    python tools/ref_benchmark.py <out dir> [SSA_AMD_DEVICES value] [--queries]
+--queries runs its query-length sweep instead (benchmark_queries.c: 36 queries of
+24-5478 residues, SW and NW at 8 and 16 bits, 10 times each; synthetic proteins
+of the published queries' lengths under their IDs).
 Writes the program's stdout and results/ log to <out dir> and a summary:
 per row the median of its 10 times and GCUPS = 513 x DB residues / time
 (the reference's formula, benchmark/scripts/evaluate_threads.r:111-117)."""
@@ -31,9 +34,19 @@ from libssa_amd import synthetic as syn  # noqa: E402
 from libssa_amd import workloads as W  # noqa: E402
 
 BIN = os.path.join(ROOT, "oracle", "_ref", "benchmark_threads_amd")
+BIN_Q = os.path.join(ROOT, "oracle", "_ref", "benchmark_queries_amd")
+# benchmark_queries.c's 36 query IDs and their lengths (residues of the
+# reference's benchmark/data/<ID> files, read there); synthetic proteins of
+# these lengths stand in for them on the GPU box
+QUERY_LENS = {"Q9UKN1": 5478, "P33450": 5147, "Q7TMA5": 4743, "P08519": 4548, "P20930": 4061, "P0C6B8": 3564,
+              "P28167": 3005, "P19096": 2504, "P04775": 2005, "Q8LLD0": 1046, "P27895": 1000, "P21177": 729,
+              "P42357": 657, "P03435": 567, "P25705": 553, "P18080": 513, "P58229": 511, "P10635": 497,
+              "P01008": 464, "Q3ZAI3": 390, "P07327": 375, "P03989": 362, "Q8ZGB4": 361, "P53765": 255,
+              "Q60341": 287, "P00762": 246, "P14942": 222, "P19930": 195, "P05013": 189, "P01111": 189,
+              "P02232": 144, "P03630": 127, "O74807": 110, "P07765": 70, "O29181": 63, "P56980": 24}
 
 
-def main(out, devices=None):
+def main(out, devices=None, program="threads"):
     os.makedirs(out, exist_ok=True)
     cfg = W.CONFIGS["sprot"]
     q = W.query(cfg)
@@ -46,28 +59,36 @@ def main(out, devices=None):
         os.makedirs(os.path.join(tmp, "results"))
         syn.write_fasta(os.path.join(tmp, "data", "uniprot_sprot.fasta"), codes, off)
         shutil.copy(os.path.join(ROOT, "tests", "golden", "data", "P18080.fasta"), os.path.join(tmp, "data", "P18080"))
+        if program == "queries":
+            for i, (qid, n) in enumerate(QUERY_LENS.items()):
+                if qid != "P18080":
+                    with open(os.path.join(tmp, "data", qid), "w") as f:
+                        f.write(f">{qid} synthetic, {n} residues\n{syn.query_string(syn.protein_query(n, 500 + i))}\n")
         env = dict(os.environ)
         if devices:
             env["SSA_AMD_DEVICES"] = devices
-        r = subprocess.run([BIN], cwd=tmp, capture_output=True, text=True, timeout=900, env=env)
+        r = subprocess.run([BIN_Q if program == "queries" else BIN], cwd=tmp, capture_output=True, text=True,
+                           timeout=1100, env=env)
         open(os.path.join(out, "stdout.txt"), "w").write(r.stdout)
         open(os.path.join(out, "stderr.txt"), "w").write(r.stderr)
         for f in os.listdir(os.path.join(tmp, "results")):
             shutil.copy(os.path.join(tmp, "results", f), os.path.join(out, "results_" + f))
         if r.returncode != 0:
             raise SystemExit(f"benchmark_threads exited with {r.returncode}: {r.stderr[-2000:]}")
-    cells = 513 * residues
-    lines = [f"DB {total + 0} sequences, {residues} residues; cells per search {cells:.4g}",
-             "row: median of 10 sw_align/nw_align times (s), GCUPS"]
+    lines = [f"DB {total + 0} sequences, {residues} residues",
+             "row: median of 10 sw_align/nw_align times (s), GCUPS (query length x DB residues / time)"]
+    nkey = 4 if program == "queries" else 5
     for ln in r.stdout.splitlines():
-        if not ln.startswith("P18080,"):
-            continue
         f = ln.split(",")
-        t = statistics.median(float(x) for x in f[5:])
-        lines.append(f"{','.join(f[:5]):34s} {t:9.5f} s {cells / t / 1e9:9.1f}")
+        if len(f) <= nkey or f[0] not in QUERY_LENS:
+            continue
+        t = statistics.median(float(x) for x in f[nkey:])
+        cells = QUERY_LENS[f[0]] * residues
+        lines.append(f"{','.join(f[:nkey]):34s} q {QUERY_LENS[f[0]]:5d} {t:9.5f} s {cells / t / 1e9:9.1f}")
     open(os.path.join(out, "summary.txt"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(args[0], args[1] if len(args) > 1 else None, "queries" if "--queries" in sys.argv else "threads")
