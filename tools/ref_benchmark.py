@@ -14,7 +14,8 @@ file the reference ships (tests/golden/data/P18080.fasta).
 
 usage (on the GPU box, after make -C oracle ref):
     python tools/ref_benchmark.py <out dir> [SSA_AMD_DEVICES value] [--queries]
---queries runs its query-length sweep instead (benchmark_queries.c: 36 queries of
+--pairwise runs benchmark_pairwise.c (one entry, one query, 10 x 10 000 calls per
+row: the per-call latency); --queries runs its query-length sweep instead (benchmark_queries.c: 36 queries of
 24-5478 residues, SW and NW at 8 and 16 bits, 10 times each; synthetic proteins
 of the published queries' lengths under their IDs).
 Writes the program's stdout and results/ log to <out dir> and a summary:
@@ -26,6 +27,7 @@ import statistics
 import subprocess
 import sys
 import tempfile
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -35,6 +37,7 @@ from libssa_amd import workloads as W  # noqa: E402
 
 BIN = os.path.join(ROOT, "oracle", "_ref", "benchmark_threads_amd")
 BIN_Q = os.path.join(ROOT, "oracle", "_ref", "benchmark_queries_amd")
+BIN_P = os.path.join(ROOT, "oracle", "_ref", "benchmark_pairwise_amd")
 # benchmark_queries.c's 36 query IDs and their lengths (residues of the
 # reference's benchmark/data/<ID> files, read there); synthetic proteins of
 # these lengths stand in for them on the GPU box
@@ -64,17 +67,51 @@ def main(out, devices=None, program="threads"):
                 if qid != "P18080":
                     with open(os.path.join(tmp, "data", qid), "w") as f:
                         f.write(f">{qid} synthetic, {n} residues\n{syn.query_string(syn.protein_query(n, 500 + i))}\n")
+        if program == "pairwise":
+            # (its DB is the one query file, its query Q3ZAI3: 10 x 10 000 calls per row)
+            shutil.copy(os.path.join(ROOT, "tests", "golden", "data", "P18080.fasta"),
+                        os.path.join(tmp, "data", "P18080.fasta"))
+            shutil.copy(os.path.join(ROOT, "tests", "golden", "data", "Q3ZAI3.fasta"),
+                        os.path.join(tmp, "data", "Q3ZAI3.fasta"))
         env = dict(os.environ)
         if devices:
             env["SSA_AMD_DEVICES"] = devices
-        r = subprocess.run([BIN_Q if program == "queries" else BIN], cwd=tmp, capture_output=True, text=True,
-                           timeout=1100, env=env)
-        open(os.path.join(out, "stdout.txt"), "w").write(r.stdout)
-        open(os.path.join(out, "stderr.txt"), "w").write(r.stderr)
+        binary = {"queries": BIN_Q, "pairwise": BIN_P}.get(program, BIN)
+        # (the program's stdout straight into the out dir: a long run shows progress)
+        # (a heartbeat line every 30 s: the program's own output is block-buffered
+        # into the file until it ends)
+        with open(os.path.join(out, "stdout.txt"), "w") as fo, open(os.path.join(out, "stderr.txt"), "w") as fe:
+            proc = subprocess.Popen([binary], cwd=tmp, stdout=fo, stderr=fe, env=env)
+            t0 = time.time()
+            while True:
+                try:
+                    proc.wait(timeout=30)
+                    break
+                except subprocess.TimeoutExpired:
+                    print(f"{os.path.basename(binary)} running, {time.time() - t0:.0f} s", flush=True)
+                    if time.time() - t0 > 1100:
+                        proc.kill()
+                        proc.wait()
+                        raise SystemExit(f"{binary} did not finish in 1100 s")
+        r = subprocess.CompletedProcess([binary], proc.returncode, open(os.path.join(out, "stdout.txt")).read(),
+                                        open(os.path.join(out, "stderr.txt")).read())
         for f in os.listdir(os.path.join(tmp, "results")):
             shutil.copy(os.path.join(tmp, "results", f), os.path.join(out, "results_" + f))
         if r.returncode != 0:
             raise SystemExit(f"benchmark_threads exited with {r.returncode}: {r.stderr[-2000:]}")
+    if program == "pairwise":
+        # rows "<SIMD>,<type>,<bits>_bit,t1..t10", each t the time of 10 000 calls
+        lines = ["one 513-residue DB entry (P18080) against Q3ZAI3 (390 aa); per row the median over 10 of",
+                 "the time of 10 000 sw_align/nw_align calls, and the time per call"]
+        for ln in r.stdout.splitlines():
+            f = ln.split(",")
+            if len(f) < 4 or not f[2].endswith("_bit"):
+                continue
+            t = statistics.median(float(x) for x in f[3:])
+            lines.append(f"{','.join(f[:3]):24s} {t:9.4f} s per 10 000 calls  {t / 1e4 * 1e6:8.1f} us per call")
+        open(os.path.join(out, "summary.txt"), "w").write("\n".join(lines) + "\n")
+        print("\n".join(lines))
+        return
     lines = [f"DB {total + 0} sequences, {residues} residues",
              "row: median of 10 sw_align/nw_align times (s), GCUPS (query length x DB residues / time)"]
     nkey = 4 if program == "queries" else 5
@@ -91,4 +128,5 @@ def main(out, devices=None, program="threads"):
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    main(args[0], args[1] if len(args) > 1 else None, "queries" if "--queries" in sys.argv else "threads")
+    prog = "queries" if "--queries" in sys.argv else "pairwise" if "--pairwise" in sys.argv else "threads"
+    main(args[0], args[1] if len(args) > 1 else None, prog)
