@@ -162,6 +162,10 @@ void ssa_amd_get_stats( ssa_amd_stats_t * out );
  *                        leaves a pair workgroup's hole (default 1; 0 measured -6 % on the Swiss-Prot form)
  *   "filter_onepass" 1|0 the device top-k filter as one launch (a decoupled look-back over its
  *                        blocks; default 1) or as three (block maxima, prefix, select)
+ *   "long_latency" 1|0   a DB of at most 256 groups (16 384 entries), a query of two strips or more:
+ *                        every group goes to the long-entry kernels when their throughput estimate
+ *                        beats the pair wave's latency (default 1; one 513-residue entry, q = 390:
+ *                        SW 1.48 -> 0.14 ms); 0: the length rules alone
  *   "plan_cache" 1|0     a search with the query and settings of one of the last four reuses
  *                        their plan (residue classes, bounds, strips; default 1); 0: plan each search
  *   "long_gate" 1|0|P    the pair kernel starts after the long-entry workgroups have (default 1;

@@ -671,6 +671,7 @@ void ssa_amd_set_option(const char* name, long value) {
     else if (!strcmp(name, "upload_kernel")) cfg().upload_kernel = (int)value;
     else if (!strcmp(name, "graph")) cfg().graph = (int)value;
     else if (!strcmp(name, "plan_cache")) cfg().plan_cache = (int)value;
+    else if (!strcmp(name, "long_latency")) cfg().long_latency = (int)value;
     else if (!strcmp(name, "filter_onepass")) cfg().filter_onepass = (int)value;
     else if (!strcmp(name, "filter_prefix_regs")) set_filter_prefix_regs((int)value);
     else print_warning("unknown option %s", name);

@@ -62,6 +62,7 @@ struct Config {
     int long_prio = 1;                    // long16 waves at raised issue priority (s_setprio 3)
     int long_pad = 1;
     int filter_onepass = 1;               // kernels.hip filter_onepass (0: three launches)
+    int long_latency = 1;                 // engine.cpp long_plan: a tiny DB's groups all go to the long kernels
     int plan_cache = 1;                   // engine.cpp cached_plan (0: plan every search)                     // 1: long-entry workgroups pad their LDS to the pair kernel's (a finished
                                           // one leaves exactly a pair workgroup's hole); 0: their own LDS only
     int long_gate = 1;                    // the tables kernel holds the pair kernel until the long-entry

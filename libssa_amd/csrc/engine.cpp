@@ -971,8 +971,16 @@ static int long16_rl(const DeviceDB& D, size_t m, bool nw, int Q, int R, int64_t
 }
 
 constexpr double kLongTypical = 4.0;   // long_plan: the length tail's multiple of the median group
+// long_plan's latency rule (tools/pairwise_probe.py, profiles/r06/ref_pairwise):
+// pair_kernel's single wave per group takes about kPairNsPerCell ns per cell
+// of its group's longest entry and its strips' rows; the long-entry kernels
+// score about kLong16CellsPerNs (SW, packed) or kLong32CellsPerNs (int32)
+// cells per ns over the whole chip, counted on the rows they pad the query to
+constexpr double kPairNsPerCell = 6.0;
+constexpr double kLong16CellsPerNs = 3400.0;
+constexpr double kLong32CellsPerNs = 2200.0;
 static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int R, int64_t minM, int64_t maxM,
-                          uint32_t scale = 1) {
+                          uint32_t scale = 1, bool nw = false, int strip_rows = 0) {
     const Config& C = cfg();
     const uint32_t need = (uint32_t)((beyond + 63) / 64);
     if (C.long_groups == 0 || D.ngroups == 0 || D.alpha > 32) return need ? UINT32_MAX : 0;
@@ -1001,6 +1009,22 @@ static uint32_t long_plan(const DeviceDB& D, size_t m, size_t beyond, int Q, int
         if (D.ngroups >= 2 * D.nsimd)
             thr = std::max(thr, (double)D.ncols_sum / D.nsimd * C.long_share_pct / 100.0 * scale);
         while (g < D.ngroups && g < kLongMaxGroups && D.group_ncols[g] > thr) g++;
+        // a DB too small to fill the chip (at most kLongMaxGroups groups): the
+        // pair launch lasts as long as its longest group's one wave walking
+        // every strip, while the long-entry kernels spread each entry over a
+        // wave of its own -- with a query of two strips or more, every group
+        // goes to them when their throughput estimate is the shorter
+        // (P18080 as the one DB entry, query Q3ZAI3: SW 1.48 -> 0.14 ms)
+        if (C.long_latency && g < D.ngroups && D.ngroups <= kLongMaxGroups && D.ngroups <= D.nsimd && strip_rows > 0 &&
+            m > (size_t)strip_rows) {
+            const size_t T = (m + strip_rows - 1) / strip_rows;
+            const double pair_ns = kPairNsPerCell * D.group_ncols[0] * (double)(T * strip_rows);
+            const int rl16 = long16_rl(D, m, nw, Q, R, minM, maxM);
+            const size_t span = rl16 > 0 ? (size_t)64 * rl16 : (size_t)256 * long_rl4(m);
+            const double padded = (double)((m + span - 1) / span * span);
+            const double long_ns = 64.0 * (double)D.ncols_sum * padded / (rl16 > 0 ? kLong16CellsPerNs : kLong32CellsPerNs);
+            if (long_ns < pair_ns) g = D.ngroups;
+        }
     }
     g = std::max(g, need);
     return need > kLongMaxGroups ? UINT32_MAX : g;
@@ -1212,7 +1236,8 @@ static void plan_view(const DeviceDB& D, const QueryView& qv, bool nw, int np, c
             // their bound covers both profiles)
             const int64_t lminM = vp.merge_mask ? std::min(minM, vp.xminM) : minM;
             const int64_t lmaxM = vp.merge_mask ? std::max(maxM, vp.xmaxM) : maxM;
-            const uint32_t lg = long_plan(D, ml, beyond, Q, R, lminM, lmaxM, force ? force->long_scale : 1u);
+            const uint32_t lg = long_plan(D, ml, beyond, Q, R, lminM, lmaxM, force ? force->long_scale : 1u, nw,
+                                        force ? 0 : 2 * pnp);
             // (an entry beyond the bound would also corrupt its group's
             // other lanes, whose padding columns run to its length: the
             // group must go to long_kernel, or the strip kernels run)

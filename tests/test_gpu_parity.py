@@ -32,8 +32,13 @@ def _counters_always():
     ask for them explicitly (option "counters" 1; by default they are computed
     only at OUTPUT_INFO, where m_run prints them)."""
     S.set_option("counters", 1)
+    # (the tests of pair-kernel plumbing use DBs small enough for long_plan's
+    # latency rule to route every group away from it: off here, on in its
+    # own test)
+    S.set_option("long_latency", 0)
     yield
     S.set_option("counters", 1)
+    S.set_option("long_latency", 1)     # (the default)
 
 
 def configure(nucleotide, spec, go, ge, chunk=1000, strands=S.FORWARD_STRAND):
@@ -320,6 +325,46 @@ def _long_entry_case(qlen, algo, gaps, waves, huge, share4=None, long16=0, kerne
             S.set_option("long16", 1)
             S.set_option("long4_share_pct", 1500)   # (the default)
         S.free_sequence(qq)
+
+
+@pytest.mark.parametrize("algo", [S.SW, S.NW])
+def test_tiny_db_routes_every_group_to_long_kernels(algo):
+    """A DB too small to fill the chip (benchmark_pairwise.c's one entry; a few
+    groups of ragged lengths): with a query of two strips or more the
+    automatic plan sends every group to the long-entry kernels (long_plan's
+    latency rule), with a one-strip query none; every score and the top hits
+    equal the oracle's either way, at one and several long passes."""
+    rng = np.random.default_rng(71)
+    S.set_option("long_latency", 1)
+    M = TABLES["matrices"][NAMES.index("blosum50")].copy()
+    configure(False, ("builtin", "blosum50"), -3, -1)
+    dbs = [np.array([513]), np.array([700, 0, 1] + list(rng.integers(1, 700, 150)))]
+    for lens in dbs:
+        lens = lens.astype(np.int64)
+        off = np.zeros(len(lens) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        codes = rng.choice(syn.AA_CODES, size=int(off[-1])).astype(np.uint8)
+        keep = np.nonzero(lens > 0)[0]
+        with tempfile.TemporaryDirectory() as tmp:
+            S.init_db(_write_db(tmp, codes, off))
+            for qlen in (30, 390, 1100):
+                q = syn.protein_query(qlen, 300 + qlen)
+                exp = po.scores(algo, q, codes, off, M, -3, -1)[keep]
+                qq = S.init_sequence_fasta(S.READ_FROM_STRING, syn.query_string(q))
+                sc, ids = _full_scores(qq, algo, len(keep))
+                assert (ids == keep).all()
+                assert (sc == exp).all(), (len(lens), qlen, np.nonzero(sc != exp)[0][:10])
+                st = S.stats()
+                assert st["kernel"].startswith("pair"), st["kernel"]
+                if qlen == 30:
+                    assert st["long_entries"] == 0
+                else:
+                    # (every group: 64 lanes each, covering every entry)
+                    assert st["long_entries"] % 64 == 0 and st["long_entries"] >= len(keep), (qlen, st["long_entries"])
+                fn = S.sw_align if algo == S.SW else S.nw_align
+                got = [(h["score"], h["id"]) for h in fn(qq, 10, 16)]
+                assert got == po.topk(exp, keep.astype(np.uint64), 10)
+                S.free_sequence(qq)
 
 
 def test_wave_timeline_and_priority_keep_scores():
