@@ -2201,6 +2201,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         std::vector<std::function<void()>> long_launch;   // the long-entry kernels' launches
         uint32_t long4 = 0;        // leading groups at 4 waves per entry, the rest of long_groups at 1
         bool long_hmm = false;     // long_kernel wrote the NW extremes (D.d_hmm)
+        bool long_only = false;    // the long-entry kernels on the search stream (below)
         size_t lds_long = pair_lds;   // LDS of a long workgroup (the pair tables' gate)
         if (long_groups > 0) {
             // a merge: the long entries are scored exactly on the compact codes
@@ -2295,12 +2296,20 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
             // (issued right after the tables kernel below: the host issues
             // the next GPU step first, and the tables kernel's gate holds the
             // pair kernel until these workgroups have started)
+            // (every group on them and of one kind: no pair work to overlap,
+            // so they run on the search stream itself, without the gate and
+            // the events across streams -- 16 us of a one-entry search's 180)
+            long_only = long_groups == D.ngroups && !fused && (long4 == 0 || long4 == long_groups);
             if (long4 > 0) {
                 la.seq0 = 0;
                 la.nseq = long4 * 64;
                 gate_total += la.nseq;                         // one workgroup per entry
                 D.gate_count += la.nseq;
                 long_launch.push_back([=, &D]() {
+                    if (long_only) {
+                        check(launch_long(la, 4, rl4, nw, st), "long kernel launch");
+                        return;
+                    }
                     check(op_wait(D.stream_long, fork_ev), "event wait");
                     check(launch_long(la, 4, rl4, nw, D.stream_long), "long kernel launch");
                     check(op_record(D.ev[7], D.stream_long), "event");
@@ -2318,10 +2327,11 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                     la.pad16 = (uint32_t)(uint16_t)(int16_t)(std::max<int64_t>(maxM, 0) - 32767);
                 }
                 long_launch.push_back([=, &D]() {
-                    check(op_wait(D.stream_long1, fork_ev), "event wait");
-                    if (rl16 > 0) check(launch_long16(la, rl16, D.stream_long1), "long kernel launch");
-                    else check(launch_long(la, 1, rl1, nw, D.stream_long1), "long kernel launch");
-                    check(op_record(D.ev[6], D.stream_long1), "event");
+                    const hipStream_t ls = long_only ? st : D.stream_long1;
+                    if (!long_only) check(op_wait(ls, fork_ev), "event wait");
+                    if (rl16 > 0) check(launch_long16(la, rl16, ls), "long kernel launch");
+                    else check(launch_long(la, 1, rl1, nw, ls), "long kernel launch");
+                    if (!long_only) check(op_record(D.ev[6], ls), "event");
                 });
             }
             if (v == 0) {
@@ -2365,7 +2375,7 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
                 const uint32_t T = main_strips + (tail_np > 0 ? 1u : 0u);
                 if (C.pair_ticket || (!no_parts && strip_parts(T) > 1)) ta.zero_ticket = gate + 1;
             }
-            if (long_groups > 0 && C.long_gate) {
+            if (long_groups > 0 && C.long_gate && !long_only) {
                 // (at most what can be resident at once: every long workgroup
                 // pads its LDS to the pair table's size, so a CU holds
                 // floor(160 KiB / that) of them -- beyond it the target is
@@ -2557,8 +2567,8 @@ static bool device_search_once(DeviceDB& D, const std::vector<QueryView>& views,
         // overflow flags, its filter pass (a fused batch defers it until the
         // one pair launch that covers every view)
         auto post = [=, &D, &kernel_bytes, &counted]() {
-            if (long4 > 0) check(op_wait(st, D.ev[7]), "event wait");
-            if (long4 < long_groups) check(op_wait(st, D.ev[6]), "event wait");
+            if (long4 > 0 && !long_only) check(op_wait(st, D.ev[7]), "event wait");
+            if (long4 < long_groups && !long_only) check(op_wait(st, D.ev[6]), "event wait");
             check(op_record(ev_k1, st, true), "event");
             if (side_tier) {
                 // (header cleared by the tables kernel; no counters)

@@ -3,7 +3,7 @@
 one DB entry, one query, many calls), with the automatic long-entry routing
 and with every group forced onto the long-entry kernels.
 
-usage (on the GPU box): python tools/pairwise_probe.py [out file]
+usage (on the GPU box): python tools/pairwise_probe.py [out file] [--one: P18080 / Q3ZAI3 only]
 Prints per (DB, query, algorithm, routing) the mean time of one
 align_free call, the device kernel time and the kernels that ran."""
 import os
@@ -24,7 +24,9 @@ S.init_gap_penalties(-3, -1)
 S.init_symbol_translation(S.AMINOACID, S.FORWARD_STRAND, 3, 3)
 S.set_thread_count(1)
 
-out = open(sys.argv[1], "w") if len(sys.argv) > 1 else None
+ONE = "--one" in sys.argv        # the P18080 / Q3ZAI3 pair only (benchmark_pairwise.c's)
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+out = open(args[0], "w") if args else None
 
 
 def say(s):
@@ -53,7 +55,9 @@ with tempfile.TemporaryDirectory() as tmp:
            ("8000 x 1-700", db(tmp, "d8k", rng.integers(1, 700, 8000), 3), 8000)]
     queries = [("Q3ZAI3 390", S.init_sequence_fasta(S.READ_FROM_FILE,
                                                     os.path.join(ROOT, "tests", "golden", "data", "Q3ZAI3.fasta")))]
-    for n in (24, 1000, 5000):
+    if ONE:
+        dbs = dbs[:1]
+    for n in (() if ONE else (24, 1000, 5000)):
         queries.append((f"synthetic {n}", S.init_sequence_fasta(S.READ_FROM_STRING,
                                                                 syn.query_string(syn.protein_query(n, 900 + n)))))
     for dname, path, nent in dbs:

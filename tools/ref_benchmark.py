@@ -52,15 +52,17 @@ QUERY_LENS = {"Q9UKN1": 5478, "P33450": 5147, "Q7TMA5": 4743, "P08519": 4548, "P
 def main(out, devices=None, program="threads"):
     os.makedirs(out, exist_ok=True)
     cfg = W.CONFIGS["sprot"]
-    q = W.query(cfg)
     total = cfg["seqs"]
-    codes, off = W.slice_db(cfg, q, total, 0, total, cfg["alphabet"])
-    codes, off = syn.with_long_tail(codes, off, cfg["long_tail"], 77, cfg["alphabet"])
-    residues = int(off[-1])
+    if program != "pairwise":      # (its DB is one query file)
+        q = W.query(cfg)
+        codes, off = W.slice_db(cfg, q, total, 0, total, cfg["alphabet"])
+        codes, off = syn.with_long_tail(codes, off, cfg["long_tail"], 77, cfg["alphabet"])
+        residues = int(off[-1])
     with tempfile.TemporaryDirectory(prefix="ssa_refbench_") as tmp:
         os.makedirs(os.path.join(tmp, "data"))
         os.makedirs(os.path.join(tmp, "results"))
-        syn.write_fasta(os.path.join(tmp, "data", "uniprot_sprot.fasta"), codes, off)
+        if program != "pairwise":
+            syn.write_fasta(os.path.join(tmp, "data", "uniprot_sprot.fasta"), codes, off)
         shutil.copy(os.path.join(ROOT, "tests", "golden", "data", "P18080.fasta"), os.path.join(tmp, "data", "P18080"))
         if program == "queries":
             for i, (qid, n) in enumerate(QUERY_LENS.items()):
